@@ -1,0 +1,162 @@
+// gpk_internal.h — shared device helpers and launcher declarations for libgpk (gfx950).
+//
+// Closed-form spectral-mixture kernel fields replacing the
+// reference's jax.grad-of-kappa machinery (code/kernel_matrix.py:49-57, :114-193).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gpk {
+
+constexpr int QMAX = 64;      // max mixture components per axis
+constexpr int PADM = 32;      // every device matrix dimension is padded to a multiple of this
+constexpr int NB = 32;        // SPD-inverse pivot block (= one 32x32 tile)
+constexpr double SQRT5 = 2.23606797749978969641;
+constexpr double TWO_PI = 6.28318530717958647692;
+
+enum Kind { SE_COS = 0, MATERN52_COS = 1, SE = 2, MATERN52 = 3 };
+
+__host__ __device__ inline bool kind_matern(int k) { return k == MATERN52_COS || k == MATERN52; }
+__host__ __device__ inline bool kind_cos(int k) { return k == SE_COS || k == MATERN52_COS; }
+inline int pad_up(int n) { return (n + PADM - 1) / PADM * PADM; }
+
+// Per-axis kernel constants, recomputed on device from the params at the start of a step.
+struct AxisConst {
+  double w[QMAX];    // e^{log-w}
+  double a[QMAX];    // e^{log-ls}   (an inverse lengthscale, kernel_matrix.py:147)
+  double om[QMAX];   // 2*pi*freq
+};
+
+// Step scalars (device), written by the prep kernel.
+struct StepScalars {
+  double tau, v;     // e^{log_tau}, e^{log_v}
+  double bc1, bc2;   // Adam bias corrections 1-b1^t, 1-b2^t for this step
+};
+
+// radial factor m(d) and derivatives; Matern52 (kernel_matrix.py:147-151) or SE (:125)
+template <bool MATERN>
+__device__ __forceinline__ void radial(double d, double a, double& m0, double& m1, double& m2) {
+  if (MATERN) {
+    double r = SQRT5 * a * d, E = exp(-r);
+    m0 = (1.0 + r + r * r * (1.0 / 3.0)) * E;
+    m1 = -(SQRT5 / 3.0) * a * r * (1.0 + r) * E;
+    m2 = (5.0 / 3.0) * a * a * (r * r - r - 1.0) * E;
+  } else {
+    double d2 = d * d, g = exp(-a * d2);
+    m0 = g;
+    m1 = -2.0 * a * d * g;
+    m2 = (4.0 * a * a * d2 - 2.0 * a) * g;
+  }
+}
+
+// radial factor plus its log-ls derivatives
+template <bool MATERN>
+__device__ __forceinline__ void radial_l(double d, double a, double& m0, double& m1, double& m2,
+                                         double& m0l, double& m1l, double& m2l) {
+  if (MATERN) {
+    double r = SQRT5 * a * d, E = exp(-r);
+    double ka = (SQRT5 / 3.0) * a, k2 = (5.0 / 3.0) * a * a;
+    double r2 = r * r;
+    m0 = (1.0 + r + r2 * (1.0 / 3.0)) * E;
+    m1 = -ka * r * (1.0 + r) * E;
+    m2 = k2 * (r2 - r - 1.0) * E;
+    m0l = -(r2 * (1.0 / 3.0)) * (1.0 + r) * E;
+    m1l = -ka * r * (2.0 + 2.0 * r - r2) * E;
+    m2l = k2 * (-r2 * r + 5.0 * r2 - 2.0 * r - 2.0) * E;
+  } else {
+    double d2 = d * d, g = exp(-a * d2);
+    m0 = g;
+    m1 = -2.0 * a * d * g;
+    m2 = (4.0 * a * a * d2 - 2.0 * a) * g;
+    m0l = -a * d2 * g;
+    m1l = (-2.0 * a * d + 2.0 * a * a * d2 * d) * g;
+    m2l = (10.0 * a * a * d2 - 2.0 * a - 4.0 * a * a * a * d2 * d2) * g;
+  }
+}
+
+}  // namespace gpk
+
+// ------------------------------------------------------------------------------------------
+// launchers (host side), one TU per kernel family
+// ------------------------------------------------------------------------------------------
+namespace gpk {
+
+struct AssembleArgs {
+  const double* x;       // coords [n] (padded buffer ok)
+  int n;                 // true size
+  int p;                 // padded size (leading dimension)
+  const AxisConst* kc;   // device
+  double jitter;
+  double* K;             // [p*p]
+  double* D;             // [p*p]
+  int deriv;             // 1 or 2 (0: K only)
+};
+hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, hipStream_t s);
+hipError_t launch_cross(int kind, int q, const double* xr, int nr, const double* xc, int nc,
+                        int ld, const AxisConst* kc, double jitter, int deriv, double* K,
+                        double* D, hipStream_t s);
+
+// SPD inverse by blocked Gauss-Jordan sweeps (pivot blocks factored in LDS).
+struct SpdArgs {
+  double* X;       // [p*p] input (assembled K), ping
+  double* Y;       // [p*p] pong
+  int p;           // padded dim (multiple of NB)
+  int n;           // true dim (pads are identity)
+  double* piv;     // [(p/NB) * NB*NB] pivot-block inverse scratch
+  double* ldet;    // [p/NB] logdet contribution of each pivot block
+  int* status;     // nonzero => not positive definite
+};
+// Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.
+hipError_t launch_spd_inverse(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
+
+// Batched fp64 MFMA GEMM with fused epilogues.
+enum Epi {
+  EPI_STORE = 0,   // C = alpha*P1 + alpha2*P2 + beta*C0
+  EPI_RESID = 1,   // C = alpha*P1 + alpha2*P2 - F (+ U(U^2-1) if ac) ; red += sum C^2
+  EPI_QUAD = 2,    // C = alpha*P1 ; red += sum C*U
+  EPI_HALFS = 3,   // C = alpha*v*P1 + 0.5*S     (v from StepScalars)
+};
+struct GemmDesc {
+  const double* A; const double* B; int lda, ldb, ta, tb;
+  const double* A2; const double* B2; int lda2, ldb2, ta2, tb2;
+  double alpha, alpha2, beta;
+  const double* C0; int ldc0;
+  double* C; int ldc;
+  int M, N, K, K2;          // padded (multiples of 32); K2 = 0 when no second product
+  int epi;
+  int ac;                   // EPI_RESID: Allen-Cahn term
+  const double* F; const double* U; int ldf; // epilogue operands
+  int vscale;               // multiply alpha by v (StepScalars) when 1
+  double* red;              // per-tile partial sums, [tiles] (nullable)
+};
+hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles,
+                             const StepScalars* sc, hipStream_t s);
+
+// GEMV y = alpha * A x (A padded p x p, op N), optional epilogues like GEMM
+struct GemvDesc {
+  const double* A; int lda; const double* x; double* y; int p; int rows;
+  double alpha;
+  int epi;           // EPI_STORE / EPI_RESID / EPI_QUAD
+  int ac;
+  const double* F; const double* U;
+  double* red;       // per-block partials
+};
+hipError_t launch_gemv(const GemvDesc& d, hipStream_t s);
+int gemv_blocks(int rows);
+
+// parameter-gradient contraction
+struct PGradArgs {
+  const double* x; int n; int p;
+  const AxisConst* kc;
+  const double* GK; const double* GD;     // 2D mode: materialised [p*p]
+  const double* Kinv;                     // 1D mode
+  const double* alpha; const double* beta; const double* R;  // 1D mode vectors
+  double halfc;                           // 1D mode: 0.5*logdet flag
+  int deriv;
+  double* part;                           // [nblocks * 3*QMAX]
+};
+hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int naxes,
+                        int blocks_per_axis, const StepScalars* sc, hipStream_t s);
+int pgrad_blocks(int n);
+
+}  // namespace gpk

@@ -1,0 +1,183 @@
+// pgrad.hip — kernel-hyperparameter gradient contraction (gfx950).
+//
+// Replaces the reverse pass that jax.grad pushes through vmap(kappa) and
+// vmap(grad(grad(kappa))) (code/kernel_matrix.py:26, :49-57; code/model_GP_solver_2d.py:179):
+//
+//   dL/dtheta_q = sum_ij G_K[i,j] dK_ij/dtheta_q + G_D[i,j] dD_ij/dtheta_q,
+//   theta in {freq, log-ls, log-w},  G_K = dL/dK, G_D = dL/dD   
+//
+// The fields depend on d = |x_i - x_j| only, so each unordered pair is evaluated once with
+// its mirror's weight folded in (D_x1's sign s_ij folded into the weight).  A workgroup
+// stages 256 pairs (d, w_K, w_D) in LDS; thread (g = t>>5, q = t&31) walks every 8th pair for
+// mixture component q, so each (pair, q) costs one exp + one sincos; 8-way LDS reduction at
+// the end leaves 3*Q deterministic partials per workgroup.
+//
+// 2D mode reads materialised G_K / G_D tiles; 1D mode forms them on the fly from K^{-1} and
+// the vectors alpha = K^{-1}u, beta = K^{-1}D^T R, R (model_GP_solver_1d.py:80-149):
+//   G_K = c/2 K^{-1} - 1/2 alpha alpha^T - v beta alpha^T,   G_D = v R alpha^T.
+#include "gpk_internal.h"
+
+namespace gpk {
+
+constexpr int PAIRS = 256;  // pairs per workgroup = 8 rows x 32 cols of a 32x32 tile
+
+struct PGradBatch {
+  PGradArgs ax[2];
+  int tiles[2];
+};
+
+template <bool MATERN, bool COS, int DERIV, bool MODE1D>
+__global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
+                                                    const StepScalars* __restrict__ sc) {
+  const int axis = blockIdx.y;
+  const PGradArgs& A = b.ax[axis];
+  const int blk = blockIdx.x;
+  const int tile = blk >> 2, chunk = blk & 3;
+  if (tile >= b.tiles[axis]) return;
+  int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+  while (I * (I + 1) / 2 > tile) --I;
+  const int J = tile - I * (I + 1) / 2;
+
+  __shared__ double sd[PAIRS], swk[PAIRS], swd[PAIRS];
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
+  __shared__ double sacc[8][3][32];
+  const int t = threadIdx.x;
+  if (t < q) {
+    sw[t] = A.kc->w[t];
+    sa[t] = A.kc->a[t];
+    so[t] = A.kc->om[t];
+  }
+  {  // stage pair t
+    const int i = I * 32 + chunk * 8 + (t >> 5), j = J * 32 + (t & 31);
+    double d = 0.0, wk = 0.0, wd = 0.0;
+    if (i < A.n && j < A.n) {
+      const double diff = A.x[i] - A.x[j];
+      d = fabs(diff);
+      const double sij = diff >= 0.0 ? 1.0 : -1.0;
+      const double sji = (A.x[j] - A.x[i]) >= 0.0 ? 1.0 : -1.0;
+      double gkij, gkji, gdij, gdji;
+      if (MODE1D) {
+        const double v = sc->v;
+        const double ai = A.alpha[i], aj = A.alpha[j];
+        gkij = A.halfc * A.Kinv[(size_t)i * A.p + j] - 0.5 * ai * aj - v * A.beta[i] * aj;
+        gkji = A.halfc * A.Kinv[(size_t)j * A.p + i] - 0.5 * aj * ai - v * A.beta[j] * ai;
+        gdij = v * A.R[i] * aj;
+        gdji = v * A.R[j] * ai;
+      } else {
+        gkij = A.GK[(size_t)i * A.p + j];
+        gkji = A.GK[(size_t)j * A.p + i];
+        gdij = A.GD[(size_t)i * A.p + j];
+        gdji = A.GD[(size_t)j * A.p + i];
+      }
+      if (DERIV == 1) {
+        gdij *= sij;
+        gdji *= sji;
+      }
+      if (I == J) {  // diagonal tile: every ordered pair once
+        wk = gkij;
+        wd = gdij;
+      } else {       // off-diagonal tile: fold in the mirror pair (j, i)
+        wk = gkij + gkji;
+        wd = gdij + gdji;
+      }
+    }
+    sd[t] = d;
+    swk[t] = wk;
+    swd[t] = wd;
+  }
+  __syncthreads();
+
+  const int g = t >> 5, ql = t & 31;
+  double* out = A.part + (size_t)blk * (3 * QMAX);
+  for (int q0 = 0; q0 < q; q0 += 32) {
+    const int c = q0 + ql;
+    double accf = 0.0, accl = 0.0, accw = 0.0;
+    if (c < q) {
+      const double a = sa[c], om = so[c];
+      for (int e = g; e < PAIRS; e += 8) {
+        const double wk = swk[e], wd = swd[e];
+        if (wk == 0.0 && wd == 0.0) continue;
+        const double d = sd[e];
+        double m0, m1, m2, m0l, m1l, m2l;
+        radial_l<MATERN>(d, a, m0, m1, m2, m0l, m1l, m2l);
+        if (COS) {
+          double S, C;
+          sincos(om * d, &S, &C);
+          const double c0 = C, c1 = -om * S, c2 = -om * om * C;
+          const double c0f = -TWO_PI * d * S;
+          const double c1f = -TWO_PI * S - TWO_PI * om * d * C;
+          const double c2f = -2.0 * TWO_PI * om * C + TWO_PI * om * om * d * S;
+          double fw = m0 * c0, fl = m0l * c0, ff = m0 * c0f;
+          double dw, dl, df;
+          if (DERIV == 2) {
+            dw = m2 * c0 + 2.0 * m1 * c1 + m0 * c2;
+            dl = m2l * c0 + 2.0 * m1l * c1 + m0l * c2;
+            df = m2 * c0f + 2.0 * m1 * c1f + m0 * c2f;
+          } else {
+            dw = m1 * c0 + m0 * c1;
+            dl = m1l * c0 + m0l * c1;
+            df = m1 * c0f + m0 * c1f;
+          }
+          accw += wk * fw + wd * dw;
+          accl += wk * fl + wd * dl;
+          accf += wk * ff + wd * df;
+        } else {
+          const double dw = DERIV == 2 ? m2 : m1, dl = DERIV == 2 ? m2l : m1l;
+          accw += wk * m0 + wd * dw;
+          accl += wk * m0l + wd * dl;
+        }
+      }
+    }
+    sacc[g][0][ql] = accf;
+    sacc[g][1][ql] = accl;
+    sacc[g][2][ql] = accw;
+    __syncthreads();
+    if (t < 96) {
+      const int which = t >> 5, qq = t & 31;
+      double s = 0.0;
+#pragma unroll
+      for (int gg = 0; gg < 8; ++gg) s += sacc[gg][which][qq];
+      if (q0 + qq < QMAX) out[which * QMAX + q0 + qq] = s;
+    }
+    __syncthreads();
+  }
+}
+
+int pgrad_blocks(int n) {
+  int T = pad_up(n) / 32;
+  return T * (T + 1) / 2 * 4;
+}
+
+template <bool MATERN, bool COS>
+static void launch_pg_t(const PGradBatch& b, int naxes, int bpa, int q, int deriv, int mode1d,
+                        const StepScalars* sc, hipStream_t s) {
+  dim3 grid(bpa, naxes);
+  if (mode1d) {
+    hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, true>), grid, dim3(256), 0, s, b, q, sc);
+  } else if (deriv == 2) {
+    hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, false>), grid, dim3(256), 0, s, b, q, sc);
+  } else {
+    hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 1, false>), grid, dim3(256), 0, s, b, q, sc);
+  }
+}
+
+hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int naxes,
+                        int blocks_per_axis, const StepScalars* sc, hipStream_t s) {
+  PGradBatch b{};
+  for (int k = 0; k < naxes; ++k) {
+    b.ax[k] = a[k];
+    int T = a[k].p / 32;
+    b.tiles[k] = T * (T + 1) / 2;
+  }
+  int deriv = a[0].deriv;
+  switch (kind) {
+    case SE_COS: launch_pg_t<false, true>(b, naxes, blocks_per_axis, q, deriv, mode1d, sc, s); break;
+    case MATERN52_COS: launch_pg_t<true, true>(b, naxes, blocks_per_axis, q, deriv, mode1d, sc, s); break;
+    case SE: launch_pg_t<false, false>(b, naxes, blocks_per_axis, q, deriv, mode1d, sc, s); break;
+    default: launch_pg_t<true, false>(b, naxes, blocks_per_axis, q, deriv, mode1d, sc, s); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace gpk

@@ -1,0 +1,62 @@
+// stepk.h — argument blocks of the step-tail kernels (loss, reductions, Adam).
+#pragma once
+#include "gpk_internal.h"
+
+namespace gpk {
+
+// Flat-parameter layout (jax pytree order, include/gpk.h) plus padded device geometry.
+struct Layout {
+  int dim, naxes, q;
+  int n1, n2, p1, p2;   // true / padded sizes (1D: n2 = p2 = 1)
+  int off_u;            // U (2D) / u (1D)
+  int off_kp[2];        // start of (freq, log-ls, log-w) per axis
+  int off_tau, off_v;
+  int off_small, nsmall;  // contiguous non-U block (kernel params + log_tau + log_v)
+  int64_t nparams;
+};
+
+struct AdamHyper {
+  double lr, b1, b2, eps;
+};
+
+struct FinalizeArgs {
+  Layout L;
+  AdamHyper hyper;
+  double llk_weight, logdet;
+  int apply, has_cos;
+  const double* red_quad; int nquad;
+  const double* red_egap; int negap;
+  const double* ldet[2]; int nldet[2];
+  const double* pg;          // reduced [naxes][3*QMAX]
+  const AxisConst* kc;
+  const StepScalars* sc;
+  const double* Up;          // padded U (2D, stride p2) / u (1D)
+  const double* bvals;
+  const int* bidx; int nb;   // 1D
+  double* params; double* grad; double* m; double* v;
+  double* losses; int* loss_slot;
+  double* diag;              // [8]: loss, logdet1, logdet2, quad, egap, bgap
+};
+
+struct AdamUArgs {
+  Layout L;
+  AdamHyper hyper;
+  double llk_weight;
+  int apply, ac;
+  const StepScalars* sc;
+  const double* E1; const double* E2; const double* R;
+  double* Up;
+  const double* bvals;
+  const int* bidx; int nb;
+  double* params; double* grad; double* m; double* v;
+};
+
+hipError_t launch_prep2(const double* params, const Layout& L, AxisConst* kc, StepScalars* sc,
+                        int* count, int apply, double b1, double b2, hipStream_t s);
+hipError_t launch_reduce_parts(const double* part, int bpa, int naxes, int q, double* out,
+                               hipStream_t s);
+hipError_t launch_finalize(const FinalizeArgs& f, hipStream_t s);
+hipError_t launch_adam_u(const AdamUArgs& a, hipStream_t s);
+hipError_t launch_sync_u(const double* params, const Layout& L, double* Up, hipStream_t s);
+
+}  // namespace gpk

@@ -1,0 +1,103 @@
+"""ctypes binding of libgpk.so (include/gpk.h).
+
+The product path has exactly one compute backend: the gfx950 HIP library.  If it is not
+built, or no gfx950 device is visible, every call raises — there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libgpk.so")
+
+GPK_OK, GPK_EINVAL, GPK_ENOTPD, GPK_EHIP, GPK_ERCCL, GPK_ENOMEM, GPK_ENODEV = range(7)
+KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}
+EQ_IDS = {"poisson": 0, "allencahn": 1, "advection": 2}
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int32)
+
+
+class GPKError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libgpk error {code}: {msg}")
+        self.code = code
+
+
+class NotPositiveDefinite(GPKError):
+    pass
+
+
+class gpk_problem(ctypes.Structure):
+    _fields_ = [
+        ("dim", ctypes.c_int32), ("eq", ctypes.c_int32), ("kind", ctypes.c_int32),
+        ("n1", ctypes.c_int32), ("n2", ctypes.c_int32), ("q", ctypes.c_int32),
+        ("x1", _dp), ("x2", _dp), ("src", _dp), ("bvals", _dp), ("bidx", _ip),
+        ("nb", ctypes.c_int32),
+        ("jitter", ctypes.c_double), ("llk_weight", ctypes.c_double),
+        ("logdet", ctypes.c_double), ("beta", ctypes.c_double),
+        ("lr", ctypes.c_double), ("b1", ctypes.c_double), ("b2", ctypes.c_double),
+        ("eps", ctypes.c_double),
+        ("device", ctypes.c_int32), ("flags", ctypes.c_int32),
+    ]
+
+
+EXPORTS = {
+    "gpk_abi_version": ([], ctypes.c_int),
+    "gpk_last_error": ([], ctypes.c_char_p),
+    "gpk_device_count": ([_ip], ctypes.c_int),
+    "gpk_kernel_matrices": ([ctypes.c_int32, ctypes.c_int32, _dp, ctypes.c_int32, _dp,
+                             ctypes.c_int32, _dp, _dp, _dp, ctypes.c_int32, ctypes.c_double,
+                             _dp, _dp], ctypes.c_int),
+    "gpk_create": ([ctypes.POINTER(gpk_problem), ctypes.c_double,
+                    ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "gpk_destroy": ([ctypes.c_void_p], ctypes.c_int),
+    "gpk_num_params": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
+    "gpk_set_params": ([ctypes.c_void_p, _dp, ctypes.c_int64], ctypes.c_int),
+    "gpk_get_params": ([ctypes.c_void_p, _dp, ctypes.c_int64], ctypes.c_int),
+    "gpk_set_opt_state": ([ctypes.c_void_p, ctypes.c_int64, _dp, _dp, ctypes.c_int64], ctypes.c_int),
+    "gpk_get_opt_state": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), _dp, _dp,
+                           ctypes.c_int64], ctypes.c_int),
+    "gpk_loss_grad": ([ctypes.c_void_p, _dp, _dp], ctypes.c_int),
+    "gpk_step": ([ctypes.c_void_p, ctypes.c_int32, _dp], ctypes.c_int),
+    "gpk_predict": ([ctypes.c_void_p, _dp, ctypes.c_int32, _dp, ctypes.c_int32, _dp], ctypes.c_int),
+    "gpk_criterion": ([ctypes.c_void_p, _dp], ctypes.c_int),
+    "gpk_profile_stages": ([ctypes.c_void_p, ctypes.c_int32, _dp, ctypes.c_int32, _ip], ctypes.c_int),
+    "gpk_stage_name": ([ctypes.c_void_p, ctypes.c_int32], ctypes.c_char_p),
+    "gpk_time_spd_inverse": ([ctypes.c_void_p, ctypes.c_int32, _dp], ctypes.c_int),
+}
+
+_LIB = None
+
+
+def load():
+    """Load libgpk.so (raises if it has not been built — no fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise GPKError(GPK_ENODEV, f"{LIB_PATH} not built; run __graft_entry__.build() "
+                                       "or `make -C gaussian-process-slover-for-high-freq-pde_amd/csrc`")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (argtypes, restype) in EXPORTS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        _LIB = lib
+    return _LIB
+
+
+def check(rc):
+    if rc != GPK_OK:
+        msg = load().gpk_last_error().decode(errors="replace")
+        if rc == GPK_ENOTPD:
+            raise NotPositiveDefinite(rc, msg)
+        raise GPKError(rc, msg)
+
+
+def dptr(a):
+    return a.ctypes.data_as(_dp)
+
+
+def f64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))

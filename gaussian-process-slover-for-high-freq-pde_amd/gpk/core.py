@@ -1,0 +1,189 @@
+"""Device-resident solver handle: the Python face of libgpk's C ABI.
+
+One `DeviceSolver` = one reference solver object (GP_solver_1d_single /
+GP_solver_2d_single / GP_solver_2d_single_advection) whose params and optax Adam state
+live in HBM on one MI355X.  Methods map 1:1 onto include/gpk.h.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, dptr, f64
+
+
+def tree_flatten(t):
+    """jax pytree leaf order for nested dicts: keys sorted (code/model_GP_solver_2d.py:245-261)."""
+    if isinstance(t, dict):
+        parts = [tree_flatten(t[k]) for k in sorted(t)]
+        return np.concatenate(parts) if parts else np.zeros(0)
+    return np.asarray(t, dtype=np.float64).reshape(-1)
+
+
+def tree_unflatten(template, flat):
+    flat = np.asarray(flat, dtype=np.float64)
+    pos = [0]
+
+    def rec(t):
+        if isinstance(t, dict):
+            return {k: rec(t[k]) for k in sorted(t)}
+        a = np.asarray(t)
+        n = a.size
+        out = flat[pos[0]:pos[0] + n].reshape(a.shape).copy()
+        pos[0] += n
+        return out if a.shape else float(out)
+
+    out = rec(template)
+    if pos[0] != flat.size:
+        raise ValueError("flat vector does not match the params template")
+    return out
+
+
+def params_template(dim, n1, n2, Q):
+    """Shapes of the reference's params pytree (train(), 1d.py:203-213 / 2d.py:245-261)."""
+    kp = {"freq": np.zeros(Q), "log-ls": np.zeros(Q), "log-w": np.zeros(Q)}
+    if dim == 1:
+        return {"kernel_paras": kp, "log_tau": 0.0, "log_v": 0.0, "u": np.zeros((n1, 1))}
+    return {"U": np.zeros((n1, n2)), "kernel_paras_1": dict(kp),
+            "kernel_paras_2": {k: v.copy() for k, v in kp.items()}, "log_tau": 0.0, "log_v": 0.0}
+
+
+class DeviceSolver:
+    def __init__(self, dim, eq, kind, x1, src, bvals, x2=None, bidx=None, Q=30, jitter=1e-6,
+                 llk_weight=200.0, logdet=True, beta=1.0, lr=0.01, freq_scale=20.0, device=0,
+                 b1=0.9, b2=0.999, eps=1e-8):
+        lib = _lib.load()
+        self.dim = int(dim)
+        self.eq = eq
+        self.kind = kind
+        self.Q = int(Q)
+        self._x1 = f64(x1).reshape(-1)
+        self.n1 = self._x1.size
+        self._x2 = f64(x2).reshape(-1) if x2 is not None else np.zeros(1)
+        self.n2 = self._x2.size if dim == 2 else 1
+        self._src = f64(src).reshape(-1)
+        self._bvals = f64(bvals).reshape(-1)
+        if self._src.size != self.n1 * self.n2:
+            raise ValueError("src must have n1*n2 entries")
+        if dim == 1:
+            self._bidx = np.ascontiguousarray(np.asarray(bidx, dtype=np.int32).reshape(-1))
+            if self._bidx.size != self._bvals.size:
+                raise ValueError("Xind and y must have the same length")
+        else:
+            self._bidx = np.zeros(1, dtype=np.int32)
+            if self._bvals.size != 2 * self.n1 + 2 * self.n2:
+                raise ValueError("2D bvals must be hstack(U[0,:],U[-1,:],U[:,0],U[:,-1])")
+        p = _lib.gpk_problem()
+        p.dim = self.dim
+        p.eq = _lib.EQ_IDS[eq]
+        p.kind = _lib.KIND_IDS[kind] if isinstance(kind, str) else int(kind)
+        p.n1, p.n2, p.q = self.n1, self.n2, self.Q
+        p.x1, p.x2, p.src, p.bvals = dptr(self._x1), dptr(self._x2), dptr(self._src), dptr(self._bvals)
+        p.bidx = self._bidx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        p.nb = self._bvals.size if dim == 1 else 0
+        p.jitter, p.llk_weight, p.logdet, p.beta = jitter, llk_weight, float(logdet), beta
+        p.lr, p.b1, p.b2, p.eps = lr, b1, b2, eps
+        p.device = device
+        self._prob = p
+        h = ctypes.c_void_p()
+        check(lib.gpk_create(ctypes.byref(p), float(freq_scale), ctypes.byref(h)))
+        self._h = h
+        n = ctypes.c_int64()
+        check(lib.gpk_num_params(h, ctypes.byref(n)))
+        self.nparams = n.value
+        self.template = params_template(self.dim, self.n1, self.n2, self.Q)
+
+    # -- lifecycle ---------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().gpk_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- params / optimizer state --------------------------------------------------------
+    def get_flat(self):
+        out = np.empty(self.nparams)
+        check(_lib.load().gpk_get_params(self._h, dptr(out), self.nparams))
+        return out
+
+    def set_flat(self, flat):
+        flat = f64(flat).reshape(-1)
+        check(_lib.load().gpk_set_params(self._h, dptr(flat), flat.size))
+
+    def get_params(self):
+        return tree_unflatten(self.template, self.get_flat())
+
+    def set_params(self, params):
+        self.set_flat(tree_flatten(params))
+
+    def get_opt_state(self):
+        mu = np.empty(self.nparams)
+        nu = np.empty(self.nparams)
+        c = ctypes.c_int64()
+        check(_lib.load().gpk_get_opt_state(self._h, ctypes.byref(c), dptr(mu), dptr(nu), self.nparams))
+        return int(c.value), mu, nu
+
+    def set_opt_state(self, count, mu, nu):
+        mu, nu = f64(mu).reshape(-1), f64(nu).reshape(-1)
+        check(_lib.load().gpk_set_opt_state(self._h, int(count), dptr(mu), dptr(nu), self.nparams))
+
+    # -- hot path ---------------------------------------------------------------------------
+    def loss_grad(self):
+        loss = ctypes.c_double()
+        g = np.empty(self.nparams)
+        check(_lib.load().gpk_loss_grad(self._h, ctypes.byref(loss), dptr(g)))
+        return loss.value, g
+
+    def step(self, n=1, losses=True):
+        out = np.empty(max(int(n), 1))
+        check(_lib.load().gpk_step(self._h, int(n), dptr(out) if losses else None))
+        return out[:n] if losses else None
+
+    def predict(self, xte1, xte2=None):
+        x1 = f64(xte1).reshape(-1)
+        if self.dim == 1:
+            out = np.empty(x1.size)
+            check(_lib.load().gpk_predict(self._h, dptr(x1), x1.size, None, 0, dptr(out)))
+            return out
+        x2 = f64(xte2).reshape(-1)
+        out = np.empty(x1.size * x2.size)
+        check(_lib.load().gpk_predict(self._h, dptr(x1), x1.size, dptr(x2), x2.size, dptr(out)))
+        return out.reshape(x1.size, x2.size)
+
+    def criterion(self):
+        c = ctypes.c_double()
+        check(_lib.load().gpk_criterion(self._h, ctypes.byref(c)))
+        return c.value
+
+    # -- measurement -----------------------------------------------------------------------
+    def profile_stages(self, iters=10):
+        lib = _lib.load()
+        cap = 16
+        out = np.zeros(cap)
+        n = ctypes.c_int32()
+        check(lib.gpk_profile_stages(self._h, int(iters), dptr(out), cap, ctypes.byref(n)))
+        return {lib.gpk_stage_name(self._h, k).decode(): float(out[k]) for k in range(n.value)}
+
+    def time_spd_inverse(self, iters=10):
+        us = ctypes.c_double()
+        check(_lib.load().gpk_time_spd_inverse(self._h, int(iters), ctypes.byref(us)))
+        return us.value
+
+
+def kernel_matrices(kind, x1, x2, paras, jitter=0.0, deriv=0):
+    """gpk_kernel_matrices: (K, D) with K = kappa(x1_i, x2_j) + jitter*[i==j]."""
+    lib = _lib.load()
+    x1, x2 = f64(x1).reshape(-1), f64(x2).reshape(-1)
+    lw, ll, fr = (f64(paras[k]).reshape(-1) for k in ("log-w", "log-ls", "freq"))
+    K = np.empty((x1.size, x2.size))
+    D = np.empty_like(K) if deriv else None
+    k = _lib.KIND_IDS[kind] if isinstance(kind, str) else int(kind)
+    check(lib.gpk_kernel_matrices(k, int(deriv), dptr(x1), x1.size, dptr(x2), x2.size, dptr(lw),
+                                  dptr(ll), dptr(fr), lw.size, float(jitter), dptr(K),
+                                  dptr(D) if deriv else None))
+    return K, D

@@ -1,0 +1,140 @@
+/*
+ * gpk.h — C ABI of libgpk, the MI355X-native (gfx950, HIP) hot path of the GP-PDE solver.
+ *
+ * The reference (xuangu-fang/Gaussian-Process-Slover-for-High-Freq-PDE, pure Python + JAX)
+ * has no FFI: its "operator surface" is a handful of Python methods.  Each entry point
+ * below replaces one of them; the Python mirror in
+ * gaussian-process-slover-for-high-freq-pde_amd/gpk/ binds them with ctypes
+ * (INTEGRATION.md shows the binding).  References are to /root/reference/code/.
+ *
+ * Conventions
+ *   - every function returns an int status (GPK_OK = 0); on failure gpk_last_error()
+ *     returns a thread-local message.  No C++ exception crosses the ABI.
+ *   - all pointers are HOST pointers unless a name ends in _dev; the library copies.
+ *   - matrices are row-major; x1 indexes rows (kernel_matrix.py:26).
+ *   - fp64 throughout (kernel_matrix.py:6-7 enables jax x64).
+ *   - one handle = one HIP device + one HIP stream; calls on a handle are synchronous on
+ *     return and not re-entrant; distinct handles are independent.
+ */
+#ifndef GPK_H_
+#define GPK_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPK_ABI_VERSION 1
+
+/* status codes */
+enum {
+  GPK_OK = 0,
+  GPK_EINVAL = 1,  /* bad argument (reference: assert / raise Exception('Invalid Kernel')) */
+  GPK_ENOTPD = 2,  /* a covariance factor lost positive definiteness in the SPD inverse   */
+  GPK_EHIP = 3,    /* HIP runtime error                                                    */
+  GPK_ERCCL = 4,   /* RCCL error (sharded handles)                                         */
+  GPK_ENOMEM = 5,  /* device allocation failed                                             */
+  GPK_ENODEV = 6   /* no gfx950 device visible                                             */
+};
+
+/* kernel kinds: kernel_matrix.py:107-193 */
+enum { GPK_SE_COS = 0, GPK_MATERN52_COS = 1, GPK_SE = 2, GPK_MATERN52 = 3 };
+
+/* equation families: model_GP_solver_1d.py:108-116, model_GP_solver_2d.py:131-141,
+ * model_GP_solver_advection.py:132-134 */
+enum { GPK_POISSON = 0, GPK_ALLENCAHN = 1, GPK_ADVECTION = 2 };
+
+/* Problem description = the solver constructor's arguments + trick_paras.
+ *   1D (GP_solver_1d_single.__init__, model_GP_solver_1d.py:38-47):
+ *       dim=1, n1=N_col, x1=X_col, src=src_col [n1], bvals=y [nb], bidx=Xind [nb]
+ *   2D / advection (GP_solver_2d_single.__init__, model_GP_solver_2d.py:40-48):
+ *       dim=2, x1=X_col[0] [n1], x2=X_col[1] [n2], src=src_vals [n1*n2],
+ *       bvals=hstack(U[0,:],U[-1,:],U[:,0],U[:,-1]) [2*n2+2*n1], bidx=NULL
+ */
+typedef struct gpk_problem {
+  int32_t dim;          /* 1 or 2 */
+  int32_t eq;           /* GPK_POISSON | GPK_ALLENCAHN | GPK_ADVECTION (dim 2 only) */
+  int32_t kind;         /* GPK_SE_COS .. GPK_MATERN52 */
+  int32_t n1, n2;       /* collocation points per axis (n2 ignored for dim 1) */
+  int32_t q;            /* mixture components Q (1..64) */
+  const double* x1;
+  const double* x2;
+  const double* src;
+  const double* bvals;
+  const int32_t* bidx;  /* dim 1 only */
+  int32_t nb;           /* dim 1: len(Xind); dim 2: ignored (2*n1+2*n2) */
+  double jitter;        /* 1e-6 in the reference (model_GP_solver_2d.py:432) */
+  double llk_weight;    /* trick_paras['llk_weight'] */
+  double logdet;        /* trick_paras['logdet'] (1.0 / 0.0) */
+  double beta;          /* advection speed (advection-sin.yaml:16); ignored otherwise */
+  double lr, b1, b2, eps; /* optax.adam(lr) defaults b1=.9, b2=.999, eps=1e-8 */
+  int32_t device;       /* HIP device ordinal */
+  int32_t flags;        /* reserved, 0 */
+} gpk_problem;
+
+typedef struct gpk_handle gpk_handle;
+
+int gpk_abi_version(void);
+const char* gpk_last_error(void);
+int gpk_device_count(int32_t* n);
+
+/* Kernel_matrix.get_kernel_matrix (kernel_matrix.py:21-30) and the vmap'd derivative
+ * covariances (model_GP_solver_2d.py:107-117, model_GP_solver_advection.py:107-117).
+ * K_out[n1*n2] = kappa(x1_i, x2_j) + jitter*[i==j]  (pass jitter=0 for the rectangular
+ * cross-covariance of preds, model_GP_solver_2d.py:198-202).
+ * deriv 1: D_out = D_x1_kappa (kernel_matrix.py:49-52); deriv 2: DD_x1_kappa (:54-57);
+ * deriv 0: D_out unused (may be NULL). */
+int gpk_kernel_matrices(int32_t kind, int32_t deriv, const double* x1, int32_t n1,
+                        const double* x2, int32_t n2, const double* logw, const double* logls,
+                        const double* freq, int32_t q, double jitter, double* K_out,
+                        double* D_out);
+
+/* Solver object: copies the problem to device memory; params start at the reference init
+ * (train(), model_GP_solver_2d.py:245-261 / model_GP_solver_1d.py:203-213) with zero Adam
+ * state.  freq_scale sets the initial frequencies linspace(0,1,Q)*freq_scale. */
+int gpk_create(const gpk_problem* prob, double freq_scale, gpk_handle** out);
+int gpk_destroy(gpk_handle* h);
+
+/* Flat parameter layout = jax's pytree leaf order (dict keys sorted):
+ *   2D: [U (n1*n2, row-major), k1.freq[Q], k1.log-ls[Q], k1.log-w[Q],
+ *        k2.freq[Q], k2.log-ls[Q], k2.log-w[Q], log_tau, log_v]
+ *   1D: [freq[Q], log-ls[Q], log-w[Q], log_tau, log_v, u[n1]]                       */
+int gpk_num_params(const gpk_handle* h, int64_t* n);
+int gpk_set_params(gpk_handle* h, const double* flat, int64_t n);
+int gpk_get_params(gpk_handle* h, double* flat, int64_t n);
+/* Adam state (optax ScaleByAdamState: count, mu, nu), same flat layout */
+int gpk_set_opt_state(gpk_handle* h, int64_t count, const double* mu, const double* nu, int64_t n);
+int gpk_get_opt_state(gpk_handle* h, int64_t* count, double* mu, double* nu, int64_t n);
+
+/* value_and_grad(loss) at the current params (model_GP_solver_2d.py:145-174,179);
+ * grad_flat may be NULL. */
+int gpk_loss_grad(gpk_handle* h, double* loss, double* grad_flat);
+
+/* n_steps x step() (model_GP_solver_2d.py:176-183): loss + full gradient + Adam update,
+ * params and Adam state device-resident.  losses[n_steps] receives the loss evaluated
+ * BEFORE each update (as step() returns it); may be NULL. */
+int gpk_step(gpk_handle* h, int32_t n_steps, double* losses);
+
+/* preds (model_GP_solver_2d.py:185-220 / model_GP_solver_1d.py:160-180) at the current
+ * params: 2D out[m1*m2] (row-major, x-test indexes rows); 1D out[m1] (xte2 ignored). */
+int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte2, int32_t m2,
+                double* out);
+
+/* compute_early_stopping (model_GP_solver_2d.py:222-233): bgap/Nb + egap/Nc */
+int gpk_criterion(gpk_handle* h, double* out);
+
+/* Per-stage device timings (HIP events on the handle's stream) of one step, averaged over
+ * `iters` eager (non-graph) steps run on a saved copy of the state: out_us[stage], names via
+ * gpk_stage_name(h, stage).  Returns #stages in *n. */
+int gpk_profile_stages(gpk_handle* h, int32_t iters, double* out_us, int32_t cap, int32_t* n);
+const char* gpk_stage_name(const gpk_handle* h, int32_t stage);
+
+/* Standalone SPD factor+inverse of the assembled K factor(s) at the current params,
+ * `iters` times on the handle's stream; returns average microseconds per call. */
+int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPK_H_ */

@@ -1,0 +1,686 @@
+"""CPU oracle for the GP-PDE log-joint step — TEST INFRASTRUCTURE ONLY.
+
+This module is a NumPy/SciPy fp64 restatement of the reference's hot path. It is used
+only by `tests/`, `__graft_entry__.smoke()` and the `cpu_baseline` leg of `bench.py`,
+always as the checker / CPU baseline, never as the product. The product path
+(`gpk`, libgpk.so) never imports it.
+
+Parity pinning: the reference (JAX 0.4.8 / optax 0.1.4) cannot run here (not installed,
+no network). The restatement is pinned by
+  (1) the reference's own committed run artefacts, replayed end to end
+      (`code/result_log/*/log.txt:2-3`: min rel-L2 error after 100 Adam steps), and
+  (2) an independent torch-autograd transcription of the reference's loss
+      (tests/test_oracle.py), which reproduces JAX's nested-`grad` derivative
+      conventions, including `abs'(0) = +1`.
+See DESIGN.md §Oracle.
+
+Reference map (paths relative to /root/reference):
+  kernels        code/kernel_matrix.py:114-193 (SE_Cos_1d, Matern52_Cos_1d, Matern52_1d, SE_1d)
+  derivatives    code/kernel_matrix.py:49-57  (D_x1_kappa, DD_x1_kappa by jax.grad)
+  assembly       code/kernel_matrix.py:21-30  (vmap(kappa) + jitter*I)
+  1D solver      code/model_GP_solver_1d.py:80-191, train :193-296, setup :299-351
+  2D solver      code/model_GP_solver_2d.py:87-233, train :235-352, setup :355-416
+  advection      code/model_GP_solver_advection.py:87-179 (D_x1, beta*U_x + U_y)
+  Adam           optax.adam(lr) defaults b1=.9 b2=.999 eps=1e-8 (model_GP_solver_2d.py:60,180-182)
+"""
+import math
+
+import numpy as np
+import scipy.linalg as sla
+
+KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}
+KIND_NAMES = {v: k for k, v in KIND_IDS.items()}
+SQRT5 = math.sqrt(5.0)
+TWO_PI = 2.0 * math.pi
+
+
+# ---- optional C helper (oracle/cpu_fields.c): same formulas, OpenMP, used for speed -------
+_CLIB = None
+_USE_C = True
+
+
+def _clib():
+    global _CLIB
+    if _CLIB is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libgpk_oracle.so")
+        if not os.path.exists(path):
+            _CLIB = False
+            return None
+        lib = ctypes.CDLL(path)
+        P = ctypes.POINTER(ctypes.c_double)
+        i, d = ctypes.c_int, ctypes.c_double
+        lib.oracle_kd.argtypes = [i, i, P, i, P, i, P, P, P, i, d, i, P, P]
+        lib.oracle_param_grad.argtypes = [i, i, P, i, P, P, P, i, P, P, P]
+        _CLIB = lib
+    return _CLIB or None
+
+
+def set_backend(use_c):
+    """use_c=False forces the pure-NumPy statement (the one tests pin first)."""
+    global _USE_C
+    _USE_C = bool(use_c)
+
+
+def _ptr(a):
+    import ctypes
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _c64(a):
+    return np.ascontiguousarray(np.asarray(a, np.float64).reshape(-1))
+
+
+def _kind_id(kind):
+    return KIND_IDS[kind] if isinstance(kind, str) else int(kind)
+
+
+def _is_matern(k):
+    return k in (1, 3)
+
+
+def _has_cos(k):
+    return k in (0, 1)
+
+
+# ----------------------------------------------------------------------------------------
+# Per-component closed forms.  d >= 0, shapes broadcast with [..., Q].
+# ----------------------------------------------------------------------------------------
+def _radial(k, d, a, want_l):
+    """m, m', m'' of the radial factor (and their d/dlog-ls when want_l).
+
+    Matern52: code/kernel_matrix.py:147-151 (r = sqrt5*d*e^{log-ls});
+    SE:       code/kernel_matrix.py:125,192   (exp(-d^2 e^{log-ls}))."""
+    if _is_matern(k):
+        r = SQRT5 * a * d
+        E = np.exp(-r)
+        m0 = (1.0 + r + r * r / 3.0) * E
+        m1 = -(SQRT5 * a / 3.0) * r * (1.0 + r) * E
+        m2 = (5.0 * a * a / 3.0) * (r * r - r - 1.0) * E
+        if not want_l:
+            return m0, m1, m2
+        m0l = -(r * r / 3.0) * (1.0 + r) * E
+        m1l = -(SQRT5 * a / 3.0) * r * (2.0 + 2.0 * r - r * r) * E
+        m2l = (5.0 * a * a / 3.0) * (-r * r * r + 5.0 * r * r - 2.0 * r - 2.0) * E
+        return m0, m1, m2, m0l, m1l, m2l
+    d2 = d * d
+    g = np.exp(-a * d2)
+    m0 = g
+    m1 = -2.0 * a * d * g
+    m2 = (4.0 * a * a * d2 - 2.0 * a) * g
+    if not want_l:
+        return m0, m1, m2
+    m0l = -a * d2 * g
+    m1l = (-2.0 * a * d + 2.0 * a * a * d2 * d) * g
+    m2l = (10.0 * a * a * d2 - 2.0 * a - 4.0 * a * a * a * d2 * d2) * g
+    return m0, m1, m2, m0l, m1l, m2l
+
+
+def _cosine(k, d, f, want_f):
+    """c, c', c'' of cos(2*pi*f*d) (and d/dfreq).  code/kernel_matrix.py:127,153."""
+    if not _has_cos(k):
+        one = np.ones_like(d * f)
+        z = np.zeros_like(one)
+        return (one, z, z, z, z, z) if want_f else (one, z, z)
+    w = TWO_PI * f
+    C = np.cos(w * d)
+    S = np.sin(w * d)
+    c0, c1, c2 = C, -w * S, -w * w * C
+    if not want_f:
+        return c0, c1, c2
+    c0f = -TWO_PI * d * S
+    c1f = -TWO_PI * S - TWO_PI * w * d * C
+    c2f = -4.0 * math.pi * w * C + TWO_PI * w * w * d * S
+    return c0, c1, c2, c0f, c1f, c2f
+
+
+def _pairs(x1, x2):
+    diff = np.asarray(x1, np.float64).reshape(-1, 1) - np.asarray(x2, np.float64).reshape(1, -1)
+    d = np.abs(diff)
+    # JAX abs JVP = select(x >= 0, g, -g) => sign(0) = +1 (SURVEY §7 "abs derivative convention")
+    s = np.where(diff >= 0.0, 1.0, -1.0)
+    return d, s
+
+
+def kernel_block(kind, x1, x2, paras, deriv=0):
+    """Row-major [n1, n2] block of kappa (deriv 0), D_x1_kappa (1) or DD_x1_kappa (2).
+
+    x1 indexes rows, x2 columns (code/kernel_matrix.py:26, code/model_GP_solver_2d.py:74-79)."""
+    k = _kind_id(kind)
+    lib = _clib() if _USE_C else None
+    if lib is not None:
+        x1c, x2c = _c64(x1), _c64(x2)
+        lw, ll, fr = _c64(paras["log-w"]), _c64(paras["log-ls"]), _c64(paras["freq"])
+        K = np.empty((x1c.size, x2c.size))
+        D = np.empty_like(K) if deriv else None
+        lib.oracle_kd(k, int(deriv), _ptr(x1c), x1c.size, _ptr(x2c), x2c.size, _ptr(lw), _ptr(ll),
+                      _ptr(fr), lw.size, 0.0, 0, _ptr(K), _ptr(D) if deriv else None)
+        return D if deriv else K
+    d, s = _pairs(x1, x2)
+    w = np.exp(np.asarray(paras["log-w"], np.float64))
+    a = np.exp(np.asarray(paras["log-ls"], np.float64))
+    f = np.asarray(paras["freq"], np.float64)
+    out = np.empty(d.shape)
+    rows = max(1, (1 << 21) // max(1, d.shape[1] * len(w)))
+    for r0 in range(0, d.shape[0], rows):
+        dd = d[r0:r0 + rows, :, None]
+        m0, m1, m2 = _radial(k, dd, a, False)
+        c0, c1, c2 = _cosine(k, dd, f, False)
+        if deriv == 0:
+            v = m0 * c0
+        elif deriv == 1:
+            v = (m1 * c0 + m0 * c1) * s[r0:r0 + rows, :, None]
+        else:
+            v = m2 * c0 + 2.0 * m1 * c1 + m0 * c2
+        out[r0:r0 + rows] = v @ w
+    return out
+
+
+def kernel_matrix(kind, x, paras, jitter):
+    """Kernel_matrix.get_kernel_matrix: vmap(kappa) + jitter*I (code/kernel_matrix.py:21-30)."""
+    K = kernel_block(kind, x, x, paras, 0)
+    K[np.diag_indices_from(K)] += jitter
+    return K
+
+
+def param_grad_contract(kind, x, paras, GK, GD, deriv):
+    """sum_ij GK[i,j] dK_ij/dtheta_q + GD[i,j] dD_ij/dtheta_q for theta in (freq, log-ls, log-w).
+
+    This is what jax.grad pushes through vmap(kappa) / vmap(grad∘grad kappa)
+    (code/kernel_matrix.py:26, :49-57). Returns dict of [Q] arrays."""
+    k = _kind_id(kind)
+    lib = _clib() if _USE_C else None
+    if lib is not None:
+        xc = _c64(x)
+        lw, ll, fr = _c64(paras["log-w"]), _c64(paras["log-ls"]), _c64(paras["freq"])
+        Q = lw.size
+        gk = _c64(GK)
+        gd = _c64(GD) if GD is not None else None
+        out = np.empty(3 * Q)
+        lib.oracle_param_grad(k, int(deriv) if GD is not None else 0, _ptr(xc), xc.size, _ptr(lw),
+                              _ptr(ll), _ptr(fr), Q, _ptr(gk), _ptr(gd) if gd is not None else None,
+                              _ptr(out))
+        return {"freq": out[:Q].copy(), "log-ls": out[Q:2 * Q].copy(), "log-w": out[2 * Q:].copy()}
+    d, s = _pairs(x, x)
+    w = np.exp(np.asarray(paras["log-w"], np.float64))
+    a = np.exp(np.asarray(paras["log-ls"], np.float64))
+    f = np.asarray(paras["freq"], np.float64)
+    Q = len(w)
+    gw = np.zeros(Q)
+    gl = np.zeros(Q)
+    gf = np.zeros(Q)
+    n2 = d.shape[1]
+    rows = max(1, (1 << 20) // max(1, n2 * Q))
+    for r0 in range(0, d.shape[0], rows):
+        sl = slice(r0, r0 + rows)
+        dd = d[sl, :, None]
+        m0, m1, m2, m0l, m1l, m2l = _radial(k, dd, a, True)
+        c0, c1, c2, c0f, c1f, c2f = _cosine(k, dd, f, True)
+        gk = GK[sl].reshape(-1)
+        gd = GD[sl].reshape(-1) if GD is not None else None
+        # K part
+        Fw = (m0 * c0).reshape(-1, Q)
+        Fl = (m0l * c0).reshape(-1, Q)
+        Ff = (m0 * c0f).reshape(-1, Q)
+        gw += gk @ Fw
+        gl += gk @ Fl
+        gf += gk @ Ff
+        if gd is not None:
+            if deriv == 2:
+                Dw = m2 * c0 + 2.0 * m1 * c1 + m0 * c2
+                Dl = m2l * c0 + 2.0 * m1l * c1 + m0l * c2
+                Df = m2 * c0f + 2.0 * m1 * c1f + m0 * c2f
+            else:
+                ss = s[sl, :, None]
+                Dw = (m1 * c0 + m0 * c1) * ss
+                Dl = (m1l * c0 + m0l * c1) * ss
+                Df = (m1 * c0f + m0 * c1f) * ss
+            gw += gd @ Dw.reshape(-1, Q)
+            gl += gd @ Dl.reshape(-1, Q)
+            gf += gd @ Df.reshape(-1, Q)
+    if not _has_cos(k):
+        gf[:] = 0.0
+    return {"freq": gf * w, "log-ls": gl * w, "log-w": gw * w}
+
+
+# ----------------------------------------------------------------------------------------
+# LU helpers mirroring jnp.linalg.solve / slogdet (LAPACK getrf + getrs) [ext]
+# ----------------------------------------------------------------------------------------
+def _lu(K):
+    return sla.lu_factor(K, check_finite=False)
+
+
+def _slogdet_from_lu(lu):
+    return float(np.sum(np.log(np.abs(np.diag(lu[0])))))
+
+
+# ----------------------------------------------------------------------------------------
+# 1D log-joint: code/model_GP_solver_1d.py:80-158
+# ----------------------------------------------------------------------------------------
+def loss_grad_1d(prob, params, want_grad=True):
+    """Negative log-joint and its gradient for GP_solver_1d_single.
+
+    prob keys: kind, x [N], src [N], xind [Nb] int, y [Nb], jitter, llk_weight, logdet, eq
+    ('poisson'|'allencahn').  params: {'kernel_paras':{freq,log-ls,log-w}, 'log_tau',
+    'log_v', 'u' [N] or [N,1]}."""
+    kind = prob["kind"]
+    x = np.asarray(prob["x"], np.float64).reshape(-1)
+    N = x.size
+    kp = params["kernel_paras"]
+    u = np.asarray(params["u"], np.float64).reshape(-1)
+    log_tau = float(params["log_tau"])
+    log_v = float(params["log_v"])
+    tau, v = math.exp(log_tau), math.exp(log_v)
+    wb = float(prob["llk_weight"])
+    c = float(prob["logdet"])
+    xind = np.asarray(prob["xind"]).reshape(-1)
+    yb = np.asarray(prob["y"], np.float64).reshape(-1)
+    f = np.asarray(prob["src"], np.float64).reshape(-1)
+    Nb = xind.size
+
+    K = kernel_matrix(kind, x, kp, prob["jitter"])          # :90
+    lu = _lu(K)
+    alpha = sla.lu_solve(lu, u)                                # :92
+    D = kernel_block(kind, x, x, kp, 2)                        # :94-96
+    uxx = D @ alpha                                            # :97
+    bres = u[xind] - yb
+    bgap = float(bres @ bres)                                  # :105-106
+    R = uxx - f
+    if prob["eq"] == "allencahn":
+        R = R + u * (u * u - 1.0)                              # :115-116
+    egap = float(R @ R)
+    logdetK = _slogdet_from_lu(lu)
+    log_prior = -0.5 * logdetK * c - 0.5 * float(u @ alpha)    # :135-137
+    log_b = 0.5 * Nb * log_tau - 0.5 * tau * bgap              # :140-142
+    eq_ll = 0.5 * N * log_v - 0.5 * v * egap                   # :145-146
+    loss = -(log_prior + log_b * wb + eq_ll)                   # :148-149
+    if not want_grad:
+        return loss, None
+    beta = sla.lu_solve(lu, D.T @ R, trans=0)
+    Kinv = sla.lu_solve(lu, np.eye(N))
+    GK = 0.5 * c * Kinv - 0.5 * np.outer(alpha, alpha) - v * np.outer(beta, alpha)
+    GD = v * np.outer(R, alpha)
+    gu = alpha + v * beta
+    if prob["eq"] == "allencahn":
+        gu = gu + v * (3.0 * u * u - 1.0) * R
+    np.add.at(gu, xind, wb * tau * bres)
+    gkp = param_grad_contract(kind, x, kp, GK, GD, 2)
+    grad = {
+        "kernel_paras": gkp,
+        "log_tau": wb * (-0.5 * Nb + 0.5 * tau * bgap),
+        "log_v": -0.5 * N + 0.5 * v * egap,
+        "u": gu.reshape(np.shape(params["u"])),
+    }
+    return loss, grad
+
+
+def preds_1d(prob, params, xte):
+    """GP_solver_1d_single.preds: Kmn K^{-1} u (code/model_GP_solver_1d.py:160-180)."""
+    kind = prob["kind"]
+    x = np.asarray(prob["x"], np.float64).reshape(-1)
+    kp = params["kernel_paras"]
+    K = kernel_matrix(kind, x, kp, prob["jitter"])
+    alpha = sla.lu_solve(_lu(K), np.asarray(params["u"], np.float64).reshape(-1))
+    Kmn = kernel_block(kind, np.asarray(xte).reshape(-1), x, kp, 0)
+    return Kmn @ alpha
+
+
+def criterion_1d(prob, params):
+    """compute_early_stopping (code/model_GP_solver_1d.py:182-191)."""
+    kind = prob["kind"]
+    x = np.asarray(prob["x"], np.float64).reshape(-1)
+    kp = params["kernel_paras"]
+    u = np.asarray(params["u"], np.float64).reshape(-1)
+    K = kernel_matrix(kind, x, kp, prob["jitter"])
+    alpha = sla.lu_solve(_lu(K), u)
+    uxx = kernel_block(kind, x, x, kp, 2) @ alpha
+    xind = np.asarray(prob["xind"]).reshape(-1)
+    bres = u[xind] - np.asarray(prob["y"]).reshape(-1)
+    R = uxx - np.asarray(prob["src"]).reshape(-1)
+    if prob["eq"] == "allencahn":
+        R = R + u * (u * u - 1.0)
+    return float(bres @ bres) / xind.size + float(R @ R) / x.size
+
+
+# ----------------------------------------------------------------------------------------
+# 2D Kronecker log-joint: code/model_GP_solver_2d.py:87-183, advection :87-179
+# ----------------------------------------------------------------------------------------
+def boundary_2d(U):
+    """u_b = hstack(U[0,:], U[-1,:], U[:,0], U[:,-1]) (code/model_GP_solver_2d.py:126)."""
+    return np.hstack((U[0, :], U[-1, :], U[:, 0], U[:, -1]))
+
+
+def _boundary_scatter(N1, N2, r):
+    g = np.zeros((N1, N2))
+    g[0, :] += r[:N2]
+    g[-1, :] += r[N2:2 * N2]
+    g[:, 0] += r[2 * N2:2 * N2 + N1]
+    g[:, -1] += r[2 * N2 + N1:]
+    return g
+
+
+def loss_grad_2d(prob, params, want_grad=True):
+    """Negative log-joint and gradient for GP_solver_2d_single / _advection.
+
+    prob keys: kind, x1 [N1], x2 [N2], src [N1,N2], bvals [2N2+2N1], jitter, llk_weight,
+    logdet, eq ('poisson'|'allencahn'|'advection'), beta (advection only).
+    params: {'U':[N1,N2], 'kernel_paras_1', 'kernel_paras_2', 'log_tau', 'log_v'}."""
+    kind = prob["kind"]
+    eq = prob["eq"]
+    x1 = np.asarray(prob["x1"], np.float64).reshape(-1)
+    x2 = np.asarray(prob["x2"], np.float64).reshape(-1)
+    N1, N2 = x1.size, x2.size
+    U = np.asarray(params["U"], np.float64).reshape(N1, N2)
+    kp1, kp2 = params["kernel_paras_1"], params["kernel_paras_2"]
+    log_tau = float(params["log_tau"])
+    log_v = float(params["log_v"])
+    tau, v = math.exp(log_tau), math.exp(log_v)
+    wb = float(prob["llk_weight"])
+    c = float(prob["logdet"])
+    F = np.asarray(prob["src"], np.float64).reshape(N1, N2)
+    bv = np.asarray(prob["bvals"], np.float64).reshape(-1)
+    Nb = bv.size
+    Nc = N1 * N2
+    deriv = 1 if eq == "advection" else 2
+    beta = float(prob.get("beta", 1.0)) if eq == "advection" else 1.0
+
+    K1 = kernel_matrix(kind, x1, kp1, prob["jitter"])        # :97-99
+    K2 = kernel_matrix(kind, x2, kp2, prob["jitter"])        # :100-102
+    lu1, lu2 = _lu(K1), _lu(K2)
+    A = sla.lu_solve(lu1, U)                                  # :104  K1^{-1} U
+    Bt = sla.lu_solve(lu2, U.T).T                             # :105  (K2^{-1} U^T)^T = U K2^{-1}
+    D1 = kernel_block(kind, x1, x1, kp1, deriv)               # :107-110
+    D2 = kernel_block(kind, x2, x2, kp2, deriv)               # :114-117
+    Uxx = D1 @ A                                              # :112
+    Uyy = Bt @ D2.T                                           # :119  (D2 K2^{-1} U^T)^T
+    ub = boundary_2d(U)
+    bres = ub - bv
+    bgap = float(bres @ bres)                                 # :126-128
+    if eq == "advection":
+        R = beta * Uxx + Uyy - F                              # advection :134
+    elif eq == "allencahn":
+        R = Uxx + Uyy + U * (U * U - 1.0) - F                 # :137-138
+    else:
+        R = Uxx + Uyy - F                                     # :133
+    egap = float(np.sum(R * R))
+    ld1, ld2 = _slogdet_from_lu(lu1), _slogdet_from_lu(lu2)
+    quad = float(np.sum(A * Bt))                              # :161  sum(K1inv_U * K2inv_Ut.T)
+    log_prior = -0.5 * N2 * ld1 * c - 0.5 * N1 * ld2 * c - 0.5 * quad
+    log_b = 0.5 * Nb * log_tau - 0.5 * tau * bgap
+    eq_ll = 0.5 * Nc * log_v - 0.5 * v * egap
+    loss = -(log_prior + log_b * wb + eq_ll)
+    if not want_grad:
+        return loss, None
+    # closed-form adjoints
+    K1inv = sla.lu_solve(lu1, np.eye(N1))
+    K2inv = sla.lu_solve(lu2, np.eye(N2))
+    S = A @ K2inv
+    X1 = K1inv @ (D1.T @ R) * beta
+    X2 = (R @ D2) @ K2inv
+    gU = S + v * (X1 + X2)
+    if eq == "allencahn":
+        gU = gU + v * (3.0 * U * U - 1.0) * R
+    gU = gU + wb * tau * _boundary_scatter(N1, N2, bres)
+    GK1 = 0.5 * c * N2 * K1inv - (0.5 * S + v * X1) @ A.T
+    GD1 = v * beta * (R @ A.T)
+    GK2 = 0.5 * c * N1 * K2inv - (0.5 * S + v * X2).T @ Bt
+    GD2 = v * (R.T @ Bt)
+    g1 = param_grad_contract(kind, x1, kp1, GK1, GD1, deriv)
+    g2 = param_grad_contract(kind, x2, kp2, GK2, GD2, deriv)
+    grad = {
+        "U": gU,
+        "kernel_paras_1": g1,
+        "kernel_paras_2": g2,
+        "log_tau": wb * (-0.5 * Nb + 0.5 * tau * bgap),
+        "log_v": -0.5 * Nc + 0.5 * v * egap,
+    }
+    return loss, grad
+
+
+def preds_2d(prob, params, xte, yte):
+    """GP_solver_2d_single.preds (code/model_GP_solver_2d.py:185-220)."""
+    kind = prob["kind"]
+    x1 = np.asarray(prob["x1"], np.float64).reshape(-1)
+    x2 = np.asarray(prob["x2"], np.float64).reshape(-1)
+    kp1, kp2 = params["kernel_paras_1"], params["kernel_paras_2"]
+    U = np.asarray(params["U"], np.float64)
+    K1 = kernel_matrix(kind, x1, kp1, prob["jitter"])
+    A = sla.lu_solve(_lu(K1), U)
+    Kmn = kernel_block(kind, np.asarray(xte).reshape(-1), x1, kp1, 0)
+    M1 = Kmn @ A
+    K2 = kernel_matrix(kind, x2, kp2, prob["jitter"])
+    M2 = sla.lu_solve(_lu(K2), M1.T)
+    Kmn2 = kernel_block(kind, np.asarray(yte).reshape(-1), x2, kp2, 0)
+    return (Kmn2 @ M2).T
+
+
+def criterion_2d(prob, params):
+    """compute_early_stopping (code/model_GP_solver_2d.py:222-233)."""
+    kind = prob["kind"]
+    eq = prob["eq"]
+    x1 = np.asarray(prob["x1"]).reshape(-1)
+    x2 = np.asarray(prob["x2"]).reshape(-1)
+    U = np.asarray(params["U"], np.float64)
+    kp1, kp2 = params["kernel_paras_1"], params["kernel_paras_2"]
+    deriv = 1 if eq == "advection" else 2
+    A = sla.lu_solve(_lu(kernel_matrix(kind, x1, kp1, prob["jitter"])), U)
+    Bt = sla.lu_solve(_lu(kernel_matrix(kind, x2, kp2, prob["jitter"])), U.T).T
+    Uxx = kernel_block(kind, x1, x1, kp1, deriv) @ A
+    Uyy = Bt @ kernel_block(kind, x2, x2, kp2, deriv).T
+    F = np.asarray(prob["src"]).reshape(U.shape)
+    if eq == "advection":
+        R = float(prob["beta"]) * Uxx + Uyy - F
+    elif eq == "allencahn":
+        R = Uxx + Uyy + U * (U * U - 1.0) - F
+    else:
+        R = Uxx + Uyy - F
+    bres = boundary_2d(U) - np.asarray(prob["bvals"]).reshape(-1)
+    return float(bres @ bres) / bres.size + float(np.sum(R * R)) / U.size
+
+
+# ----------------------------------------------------------------------------------------
+# optax.adam (0.1.4) — scale_by_adam + scale(-lr) + apply_updates  [ext]
+# ----------------------------------------------------------------------------------------
+class Adam:
+    def __init__(self, lr, b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0):
+        self.lr, self.b1, self.b2, self.eps, self.eps_root = lr, b1, b2, eps, eps_root
+
+    def init(self, params):
+        z = _tree_map(lambda p: np.zeros_like(np.asarray(p, np.float64)), params)
+        return {"count": 0, "mu": z, "nu": _tree_map(lambda p: p.copy(), z)}
+
+    def update(self, grads, state, params):
+        b1, b2 = self.b1, self.b2
+        mu = _tree_map2(lambda g, t: (1.0 - b1) * g + b1 * t, grads, state["mu"])
+        nu = _tree_map2(lambda g, t: (1.0 - b2) * (g ** 2) + b2 * t, grads, state["nu"])
+        count = state["count"] + 1
+        bc1 = 1.0 - b1 ** count
+        bc2 = 1.0 - b2 ** count
+        mu_hat = _tree_map(lambda t: t / bc1, mu)
+        nu_hat = _tree_map(lambda t: t / bc2, nu)
+        upd = _tree_map2(lambda m, n: m / (np.sqrt(n + self.eps_root) + self.eps), mu_hat, nu_hat)
+        upd = _tree_map(lambda u: u * (-self.lr), upd)
+        new_params = _tree_map2(lambda p, u: np.asarray(p, np.float64) + u, params, upd)
+        return new_params, {"count": count, "mu": mu, "nu": nu}
+
+
+def _tree_map(fn, t):
+    if isinstance(t, dict):
+        return {k: _tree_map(fn, v) for k, v in t.items()}
+    return fn(np.asarray(t, np.float64))
+
+
+def _tree_map2(fn, a, b):
+    if isinstance(a, dict):
+        return {k: _tree_map2(fn, a[k], b[k]) for k in a}
+    return fn(np.asarray(a, np.float64), np.asarray(b, np.float64))
+
+
+def _flatten(t):
+    """jax pytree leaf order: dict keys sorted (code/model_GP_solver_2d.py:245-261)."""
+    if isinstance(t, dict):
+        return np.concatenate([_flatten(t[k]) for k in sorted(t)]) if t else np.zeros(0)
+    return np.asarray(t, np.float64).reshape(-1)
+
+
+def flatten_params(params):
+    return _flatten(params)
+
+
+def unflatten_params(template, flat):
+    flat = np.asarray(flat, np.float64)
+    pos = [0]
+
+    def rec(t):
+        if isinstance(t, dict):
+            return {k: rec(t[k]) for k in sorted(t)}
+        a = np.asarray(t)
+        n = a.size
+        out = flat[pos[0]:pos[0] + n].reshape(a.shape)
+        pos[0] += n
+        return out if a.shape else float(out)
+
+    return rec(template)
+
+
+# ----------------------------------------------------------------------------------------
+# Problem setup (code/model_GP_solver_1d.py:299-351, code/model_GP_solver_2d.py:355-416)
+# ----------------------------------------------------------------------------------------
+def _u1d(name):
+    s, c = np.sin, np.cos
+    table = {
+        "poisson_1d-mix_sin": (lambda x: s(x) + 0.1 * s(20 * x) + 0.05 * s(100 * x),
+                               lambda x: -s(x) - 40.0 * s(20 * x) - 500.0 * s(100 * x)),
+        "poisson_1d-single_sin": (lambda x: s(100 * x), lambda x: -1e4 * s(100 * x)),
+        "poisson_1d-sin_cos": (lambda x: s(6 * x) * c(100 * x),
+                               lambda x: -10036.0 * s(6 * x) * c(100 * x) - 1200.0 * c(6 * x) * s(100 * x)),
+        "poisson_1d-x_time_sinx": (lambda x: x * s(200 * x),
+                                   lambda x: 400.0 * c(200 * x) - 40000.0 * x * s(200 * x)),
+        "poisson_1d-x2_add_sinx": (lambda x: s(500 * x) - 2 * (x - 0.5) ** 2,
+                                   lambda x: -250000.0 * s(500 * x) - 4.0),
+    }
+    base = name.replace("allencahn_1d", "poisson_1d")
+    return table[base]
+
+
+def equation_1d(name):
+    """(u, src) for the 1D equation_dict (code/model_GP_solver_1d.py:313-332) with analytic
+    second derivatives in place of jax.grad(grad(u)) (:299-307)."""
+    u, uxx = _u1d(name)
+    if name.startswith("allencahn_1d"):
+        return u, (lambda x: uxx(x) + u(x) * (u(x) ** 2 - 1.0))
+    return u, uxx
+
+
+def _u2d(name, beta=None):
+    s, c = np.sin, np.cos
+    if name == "poisson_2d-sin_sin":
+        return (lambda x, y: s(100 * x) * s(100 * y)), (lambda x, y: -2e4 * s(100 * x) * s(100 * y))
+    if name == "poisson_2d-sin_cos":
+        return (lambda x, y: s(100 * x) * c(100 * y)), (lambda x, y: -2e4 * s(100 * x) * c(100 * y))
+    if name == "poisson_2d-sin_add_cos":
+        g = lambda t: s(6 * t) * c(20 * t)
+        g2 = lambda t: -436.0 * s(6 * t) * c(20 * t) - 240.0 * c(6 * t) * s(20 * t)
+        return (lambda x, y: g(x) + g(y)), (lambda x, y: g2(x) + g2(y))
+    if name == "allencahn_2d-mix-sincos":
+        g = lambda t: s(t) + 0.1 * s(20 * t) + c(100 * t)
+        g2 = lambda t: -s(t) - 40.0 * s(20 * t) - 1e4 * c(100 * t)
+        u = lambda x, y: g(x) * g(y)
+        return u, (lambda x, y: g2(x) * g(y) + g(x) * g2(y) + u(x, y) * (u(x, y) ** 2 - 1.0))
+    if name == "advection-sin":
+        # beta*u_x + u_y of sin(x - beta*y) is identically 0 (advection :354-362, :386-388)
+        return (lambda x, y: s(x - beta * y)), (lambda x, y: 0.0 * x * y)
+    if name == "advection-multiscale":
+        # synthetic multi-scale source for BASELINE config C5:
+        # u = sin(x - beta*y) + 0.1 sin(20 pi x) sin(2 pi y); F = beta*u_x + u_y
+        u = lambda x, y: s(x - beta * y) + 0.1 * s(20 * np.pi * x) * s(2 * np.pi * y)
+        F = lambda x, y: (beta * 0.1 * 20 * np.pi * c(20 * np.pi * x) * s(2 * np.pi * y)
+                          + 0.1 * s(20 * np.pi * x) * 2 * np.pi * c(2 * np.pi * y))
+        return u, F
+    raise KeyError(name)
+
+
+def setup_1d(equation, n_col, scale, kind, jitter=1e-6, llk_weight=200.0, logdet=True, m_test=300):
+    """Replicates test() of code/model_GP_solver_1d.py:334-354."""
+    u, src = equation_1d(equation)
+    X_test = np.linspace(0, 1, num=m_test).reshape(-1, 1) * scale
+    Y_test = u(X_test)
+    X_col = np.linspace(0, 1, num=n_col).reshape(-1, 1) * scale
+    Xind = np.array([0, X_col.shape[0] - 1])
+    y = np.array([u(X_col[Xind[0]]), u(X_col[Xind[1]])]).reshape(-1)
+    prob = dict(kind=kind, x=X_col.reshape(-1), src=src(X_col.reshape(-1)), xind=Xind, y=y,
+                jitter=jitter, llk_weight=llk_weight, logdet=float(logdet),
+                eq=equation.split("-")[0].replace("_1d", ""))
+    return prob, X_test, Y_test
+
+
+def setup_2d(equation, n_col, scale, kind, jitter=1e-6, llk_weight=200.0, logdet=True, beta=None,
+             m_test=300, n_col2=None):
+    """Replicates test() of code/model_GP_solver_2d.py:382-416 (and advection :380-410)."""
+    u, src = _u2d(equation, beta)
+    n2 = n_col if n_col2 is None else n_col2
+    xt = np.linspace(0, 1, num=m_test) * scale
+    yt = np.linspace(0, 1, num=m_test) * scale
+    u_test = u(*np.meshgrid(xt, yt, indexing="ij"))
+    x1 = np.linspace(0, 1, num=n_col) * scale
+    x2 = np.linspace(0, 1, num=n2) * scale
+    xm, ym = np.meshgrid(x1, x2, indexing="ij")
+    u_mh = u(xm, ym)
+    bvals = boundary_2d(u_mh)
+    F = src(xm, ym) * np.ones_like(xm)
+    eqt = equation.split("-")[0]
+    eq = {"poisson_2d": "poisson", "allencahn_2d": "allencahn", "advection": "advection"}[eqt]
+    prob = dict(kind=kind, x1=x1, x2=x2, src=F, bvals=bvals, jitter=jitter,
+                llk_weight=llk_weight, logdet=float(logdet), eq=eq)
+    if eq == "advection":
+        prob["beta"] = float(beta)
+    return prob, (xt, yt), u_test
+
+
+def init_params_1d(n, Q, freq_scale):
+    """train() init, code/model_GP_solver_1d.py:203-213."""
+    return {
+        "log_tau": 0.0,
+        "log_v": 0.0,
+        "kernel_paras": {"log-w": np.log(1 / Q) * np.ones(Q), "log-ls": np.zeros(Q),
+                         "freq": np.linspace(0, 1, Q) * freq_scale},
+        "u": np.zeros((n, 1)),
+    }
+
+
+def init_params_2d(n1, n2, Q, freq_scale):
+    """train() init, code/model_GP_solver_2d.py:245-261."""
+    kp = lambda: {"log-w": np.log(1 / Q) * np.ones(Q), "log-ls": np.zeros(Q),
+                  "freq": np.linspace(0, 1, Q) * freq_scale}
+    return {"log_tau": 0.0, "log_v": 0.0, "kernel_paras_1": kp(), "kernel_paras_2": kp(),
+            "U": np.zeros((n1, n2))}
+
+
+def train_replay(dim, prob, params, lr, nepoch, test, record_every=None):
+    """Replays train() (code/model_GP_solver_1d.py:234-276 / code/model_GP_solver_2d.py:285-332):
+    step, then every nepoch/20 iterations record log(loss) (if >1), rel-L2 err, min err."""
+    opt = Adam(lr)
+    state = opt.init(params)
+    rec = {"loss_list": [], "err_list": [], "epoch_list": []}
+    min_err = 2.0
+    every = nepoch / 20 if record_every is None else record_every
+    for i in range(nepoch):
+        if dim == 1:
+            loss, g = loss_grad_1d(prob, params)
+        else:
+            loss, g = loss_grad_2d(prob, params)
+        params, state = opt.update(g, state, params)
+        if i % every == 0:
+            if dim == 1:
+                pred = preds_1d(prob, params, test[0])
+            else:
+                pred = preds_2d(prob, params, test[0][0], test[0][1])
+            ute = np.asarray(test[1])
+            err = np.linalg.norm(pred.reshape(-1) - ute.reshape(-1)) / np.linalg.norm(ute.reshape(-1))
+            min_err = min(min_err, err)
+            rec["loss_list"].append(math.log(loss) if loss > 1 else loss)
+            rec["err_list"].append(err)
+            rec["epoch_list"].append(i)
+    rec["min_err"] = min_err
+    return params, state, rec

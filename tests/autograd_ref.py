@@ -1,0 +1,127 @@
+"""Independent torch-autograd transcription of the reference's loss (test infrastructure).
+
+This mirrors the reference's own computation path rather than the closed forms:
+kappa as written in code/kernel_matrix.py:114-193, derivative covariances by nested autograd
+(as jax.grad(grad(kappa)) at code/kernel_matrix.py:49-57), jnp.abs with JAX's JVP convention
+select(x >= 0, g, -g), LU solve + slogdet, and reverse-mode autodiff for the full gradient
+(code/model_GP_solver_2d.py:87-179, code/model_GP_solver_1d.py:80-154).  It checks the
+closed-form adjoints of oracle/gp_oracle.py independently.
+"""
+import math
+
+import numpy as np
+import torch
+
+torch.set_default_dtype(torch.float64)
+
+
+def _jax_abs(x):
+    return torch.where(x >= 0, x, -x)  # autograd: select(x >= 0, g, -g), like jax's abs JVP
+
+
+def kappa(kind, x1, y1, p):
+    """Elementwise kappa over flattened pairs; p: dict of [Q] tensors."""
+    d = _jax_abs(x1 - y1)[:, None]
+    lw, ll, fr = p["log-w"][None, :], p["log-ls"][None, :], p["freq"][None, :]
+    if kind == "SE_Cos_1d":       # kernel_matrix.py:114-128
+        v = torch.exp(lw) * torch.exp(-d ** 2 * torch.exp(ll)) * torch.cos(2 * math.pi * d * fr)
+    elif kind == "Matern52_Cos_1d":  # :138-155
+        matern = (1 + math.sqrt(5) * d * torch.exp(ll) + 5 / 3 * d ** 2 * torch.exp(ll) ** 2) * \
+            torch.exp(-math.sqrt(5) * d * torch.exp(ll))
+        v = torch.exp(lw) * matern * torch.cos(2 * math.pi * d * fr)
+    elif kind == "Matern52_1d":   # :163-176
+        v = torch.exp(lw) * (1 + math.sqrt(5) * d * torch.exp(ll) + 5 / 3 * d ** 2 * torch.exp(ll) ** 2) * \
+            torch.exp(-math.sqrt(5) * d * torch.exp(ll))
+    else:                         # SE_1d :184-193
+        v = torch.exp(lw) * torch.exp(-d ** 2 * torch.exp(ll))
+    return v.sum(1)
+
+
+def mats(kind, x, p, jitter, deriv):
+    n = x.numel()
+    X1 = x.reshape(-1, 1).expand(n, n).reshape(-1).clone().requires_grad_(True)
+    X2 = x.reshape(1, -1).expand(n, n).reshape(-1)
+    k = kappa(kind, X1, X2, p)
+    K = k.reshape(n, n) + jitter * torch.eye(n)
+    g1, = torch.autograd.grad(k.sum(), X1, create_graph=True)
+    if deriv == 1:
+        D = g1
+    else:
+        D, = torch.autograd.grad(g1.sum(), X1, create_graph=True)
+    return K, D.reshape(n, n)
+
+
+def _tp(params):
+    out = {}
+    for k, v in params.items():
+        if isinstance(v, dict):
+            out[k] = _tp(v)
+        else:
+            out[k] = torch.tensor(np.asarray(v, np.float64), requires_grad=True)
+    return out
+
+
+def _grads(tp):
+    out = {}
+    for k, v in tp.items():
+        out[k] = _grads(v) if isinstance(v, dict) else (v.grad.numpy().copy() if v.grad is not None else np.zeros(v.shape))
+    return out
+
+
+def loss_grad_2d(prob, params):
+    tp = _tp(params)
+    kind, eq = prob["kind"], prob["eq"]
+    x1 = torch.tensor(prob["x1"])
+    x2 = torch.tensor(prob["x2"])
+    U = tp["U"]
+    deriv = 1 if eq == "advection" else 2
+    K1, D1 = mats(kind, x1, tp["kernel_paras_1"], prob["jitter"], deriv)
+    K2, D2 = mats(kind, x2, tp["kernel_paras_2"], prob["jitter"], deriv)
+    A = torch.linalg.solve(K1, U)
+    Bt_T = torch.linalg.solve(K2, U.T)
+    Uxx = D1 @ A
+    Uyy = (D2 @ Bt_T).T
+    ub = torch.cat((U[0, :], U[-1, :], U[:, 0], U[:, -1]))
+    bv = torch.tensor(prob["bvals"])
+    bgap = ((ub - bv) ** 2).sum()
+    F = torch.tensor(prob["src"])
+    if eq == "advection":
+        R = prob["beta"] * Uxx + Uyy - F
+    elif eq == "allencahn":
+        R = Uxx + Uyy + U * (U ** 2 - 1) - F
+    else:
+        R = Uxx + Uyy - F
+    egap = (R ** 2).sum()
+    N1, N2 = U.shape
+    c = prob["logdet"]
+    log_prior = -0.5 * N2 * torch.linalg.slogdet(K1)[1] * c - 0.5 * N1 * torch.linalg.slogdet(K2)[1] * c \
+        - 0.5 * (A * Bt_T.T).sum()
+    log_b = 0.5 * ub.numel() * tp["log_tau"] - 0.5 * torch.exp(tp["log_tau"]) * bgap
+    eq_ll = 0.5 * N1 * N2 * tp["log_v"] - 0.5 * torch.exp(tp["log_v"]) * egap
+    loss = -(log_prior + log_b * prob["llk_weight"] + eq_ll)
+    loss.backward()
+    return float(loss), _grads(tp)
+
+
+def loss_grad_1d(prob, params):
+    tp = _tp(params)
+    kind = prob["kind"]
+    x = torch.tensor(prob["x"])
+    u = tp["u"]
+    K, D = mats(kind, x, tp["kernel_paras"], prob["jitter"], 2)
+    alpha = torch.linalg.solve(K, u)
+    uxx = D @ alpha
+    xind = torch.tensor(np.asarray(prob["xind"]))
+    bgap = ((u[xind].reshape(-1) - torch.tensor(prob["y"])) ** 2).sum()
+    f = torch.tensor(prob["src"])
+    if prob["eq"] == "allencahn":
+        R = uxx.reshape(-1) + (u * (u ** 2 - 1)).reshape(-1) - f
+    else:
+        R = uxx.reshape(-1) - f
+    egap = (R ** 2).sum()
+    log_prior = -0.5 * torch.linalg.slogdet(K)[1] * prob["logdet"] - 0.5 * (u * alpha).sum()
+    log_b = 0.5 * xind.numel() * tp["log_tau"] - 0.5 * torch.exp(tp["log_tau"]) * bgap
+    eq_ll = 0.5 * x.numel() * tp["log_v"] - 0.5 * torch.exp(tp["log_v"]) * egap
+    loss = -(log_prior + log_b * prob["llk_weight"] + eq_ll)
+    loss.backward()
+    return float(loss), _grads(tp)

@@ -1,0 +1,52 @@
+"""Shared problem builders for the parity tests (test infrastructure)."""
+import numpy as np
+
+from oracle import gp_oracle as O
+
+
+def rand_kp(rng, Q, fs):
+    return {"freq": np.linspace(0, 1, Q) * fs + 0.3 * rng.normal(size=Q),
+            "log-ls": 0.3 * rng.normal(size=Q),
+            "log-w": np.log(1.0 / Q) + 0.3 * rng.normal(size=Q)}
+
+
+def problem_1d(eq="poisson", kind="Matern52_Cos_1d", n=40, Q=5, seed=0, scale=2 * np.pi, fs=20.0):
+    name = {"poisson": "poisson_1d-single_sin", "allencahn": "allencahn_1d-single_sin"}[eq]
+    prob, Xte, Yte = O.setup_1d(name, n, scale, kind)
+    rng = np.random.default_rng(seed)
+    params = {"kernel_paras": rand_kp(rng, Q, fs), "log_tau": 0.2, "log_v": -0.1,
+              "u": 0.1 * rng.normal(size=(n, 1))}
+    return prob, params, (Xte, Yte)
+
+
+def problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=24, n2=20, Q=5, seed=0, fs=20.0):
+    if eq == "advection":
+        prob, Xte, ute = O.setup_2d("advection-multiscale", n1, 1.0, kind, llk_weight=500.0,
+                                    beta=200.0, n_col2=n2, m_test=30)
+        fs = 40.0
+    elif eq == "allencahn":
+        prob, Xte, ute = O.setup_2d("allencahn_2d-mix-sincos", n1, 1.0, kind, n_col2=n2, m_test=30)
+        fs = 30.0
+    else:
+        prob, Xte, ute = O.setup_2d("poisson_2d-sin_sin", n1, 2 * np.pi, kind, n_col2=n2, m_test=30)
+    rng = np.random.default_rng(seed)
+    params = {"U": 0.1 * rng.normal(size=(n1, n2)), "kernel_paras_1": rand_kp(rng, Q, fs),
+              "kernel_paras_2": rand_kp(rng, Q, fs), "log_tau": 0.2, "log_v": -0.1}
+    return prob, params, (Xte, ute), fs
+
+
+def device_solver(prob, Q, fs=20.0, lr=0.01):
+    from gpk.core import DeviceSolver
+    if "x" in prob:
+        return DeviceSolver(1, prob["eq"], prob["kind"], prob["x"], prob["src"], prob["y"],
+                            bidx=prob["xind"], Q=Q, jitter=prob["jitter"],
+                            llk_weight=prob["llk_weight"], logdet=prob["logdet"], lr=lr,
+                            freq_scale=fs)
+    return DeviceSolver(2, prob["eq"], prob["kind"], prob["x1"], prob["src"], prob["bvals"],
+                        x2=prob["x2"], Q=Q, jitter=prob["jitter"], llk_weight=prob["llk_weight"],
+                        logdet=prob["logdet"], beta=prob.get("beta", 1.0), lr=lr, freq_scale=fs)
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))

@@ -1,0 +1,170 @@
+"""GPU parity: libgpk (HIP, gfx950) vs the CPU oracle on identical seeded inputs.
+
+Tolerances (SURVEY.md §8(c) parity contract):
+  K, D blocks             <= 1e-13 relative (max-abs / max)
+  loss, full gradient     <= max(1e-10, 50 cond(K) eps) relative (cond_tol)
+  predictions             <= 1e-10 relative
+  short Adam trajectories <= 1e-9 relative
+"""
+import numpy as np
+import pytest
+
+from oracle import gp_oracle as O
+from tests.helpers import device_solver, problem_1d, problem_2d, rel
+
+pytestmark = pytest.mark.gpu
+
+KINDS = ["SE_Cos_1d", "Matern52_Cos_1d", "SE_1d", "Matern52_1d"]
+
+
+@pytest.fixture(autouse=True)
+def _numpy_oracle():
+    O.set_backend(False)  # pin against the pure-NumPy statement
+    yield
+    O.set_backend(True)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("deriv", [0, 1, 2])
+def test_kernel_matrices(kind, deriv):
+    from gpk.core import kernel_matrices
+    rng = np.random.default_rng(3)
+    x1 = np.sort(rng.uniform(0, 3, 37))
+    x2 = np.sort(rng.uniform(0, 3, 29))
+    x2[4] = x1[7]  # a zero distance off the diagonal exercises abs'(0) = +1
+    kp = {"log-w": rng.normal(size=5) - 1, "log-ls": rng.normal(size=5), "freq": rng.uniform(0, 5, 5)}
+    K, D = kernel_matrices(kind, x1, x2, kp, 0.0, deriv)
+    assert rel(K, O.kernel_block(kind, x1, x2, kp, 0)) < 1e-13
+    if deriv:
+        assert rel(D, O.kernel_block(kind, x1, x2, kp, deriv)) < 1e-13
+
+
+def test_kernel_matrix_square_jitter():
+    from gpk.core import kernel_matrices
+    x = np.linspace(0, 1, 50) * 2 * np.pi
+    Q = 30
+    kp = {"log-w": np.log(1 / Q) * np.ones(Q), "log-ls": np.zeros(Q), "freq": np.linspace(0, 1, Q) * 20}
+    K, D = kernel_matrices("Matern52_Cos_1d", x, x, kp, 1e-6, 2)
+    assert rel(K, O.kernel_matrix("Matern52_Cos_1d", x, kp, 1e-6)) < 1e-13
+    assert rel(D, O.kernel_block("Matern52_Cos_1d", x, x, kp, 2)) < 1e-13
+    # jax abs'(0)=+1 convention: diagonal of DD is k''(0) = sum w(-5a^2/3 - omega^2)
+    w, om = np.exp(kp["log-w"]), 2 * np.pi * kp["freq"]
+    assert np.allclose(np.diag(D), np.sum(w * (-5.0 / 3.0 - om ** 2)), rtol=1e-13)
+
+
+def cond_tol(prob, params, floor=1e-10, factor=50.0):
+    """max(floor, factor * cond(K) * eps): GPU and LU/autograd references agree to this order;
+    the explicit-inverse path and LU differ by O(cond * eps) (tools/diag_parity.py)."""
+    if "x" in prob:
+        c = np.linalg.cond(O.kernel_matrix(prob["kind"], prob["x"], params["kernel_paras"], prob["jitter"]))
+    else:
+        c = max(np.linalg.cond(O.kernel_matrix(prob["kind"], prob["x1"], params["kernel_paras_1"], prob["jitter"])),
+                np.linalg.cond(O.kernel_matrix(prob["kind"], prob["x2"], params["kernel_paras_2"], prob["jitter"])))
+    return max(floor, factor * c * np.finfo(np.float64).eps)
+
+
+def _cmp_lossgrad(prob, params, Q, fs, tol=None):
+    tol = cond_tol(prob, params) if tol is None else tol
+    s = device_solver(prob, Q, fs)
+    s.set_params(params)
+    loss, g = s.loss_grad()
+    if "x" in prob:
+        lo, go = O.loss_grad_1d(prob, params)
+    else:
+        lo, go = O.loss_grad_2d(prob, params)
+    gflat = O.flatten_params(go)
+    assert abs(loss - lo) / abs(lo) < tol, (loss, lo)
+    gd = O.unflatten_params(params, g)
+    for key in sorted(go):
+        a, b = O.flatten_params(gd[key]), O.flatten_params(go[key])
+        assert rel(a, b) < tol, (key, rel(a, b))
+    assert rel(g, gflat) < tol
+    s.close()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("eq", ["poisson", "allencahn"])
+def test_loss_grad_1d(kind, eq):
+    prob, params, _ = problem_1d(eq=eq, kind=kind, n=40, Q=5, seed=1)
+    _cmp_lossgrad(prob, params, 5, 20.0)
+
+
+def test_loss_grad_1d_large():
+    prob, params, _ = problem_1d(n=200, Q=30, seed=2)  # C1 size, pads 200 -> 224
+    _cmp_lossgrad(prob, params, 30, 20.0)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("eq", ["poisson", "allencahn", "advection"])
+def test_loss_grad_2d(kind, eq):
+    prob, params, _, fs = problem_2d(eq=eq, kind=kind, n1=40, n2=36, Q=5, seed=4)
+    _cmp_lossgrad(prob, params, 5, fs)
+
+
+def test_loss_grad_2d_c3_shape():
+    prob, params, _, fs = problem_2d(eq="poisson", kind="SE_Cos_1d", n1=128, n2=128, Q=30, seed=5)
+    _cmp_lossgrad(prob, params, 30, fs)
+
+
+@pytest.mark.parametrize("dim", [1, 2])
+def test_adam_trajectory(dim):
+    if dim == 1:
+        prob, params, _ = problem_1d(n=64, Q=8, seed=6)
+        fs = 20.0
+    else:
+        prob, params, _, fs = problem_2d(n1=48, n2=40, Q=8, seed=6)
+    s = device_solver(prob, params_q(params), fs)
+    s.set_params(params)
+    losses = s.step(5)
+    opt = O.Adam(0.01)
+    st = opt.init(params)
+    p = params
+    ref_losses = []
+    for _ in range(5):
+        lo, g = (O.loss_grad_1d if dim == 1 else O.loss_grad_2d)(prob, p)
+        ref_losses.append(lo)
+        p, st = opt.update(g, st, p)
+    assert rel(losses, ref_losses) < 1e-9
+    assert rel(s.get_flat(), O.flatten_params(p)) < 1e-9
+    cnt, mu, nu = s.get_opt_state()
+    assert cnt == 5
+    assert rel(mu, O.flatten_params(st["mu"])) < 1e-8
+    s.close()
+
+
+def params_q(params):
+    kp = params.get("kernel_paras", params.get("kernel_paras_1"))
+    return len(kp["freq"])
+
+
+@pytest.mark.parametrize("dim", [1, 2])
+def test_predict_and_criterion(dim):
+    if dim == 1:
+        prob, params, (Xte, Yte) = problem_1d(n=64, Q=8, seed=7)
+        s = device_solver(prob, 8)
+        s.set_params(params)
+        pred = s.predict(Xte)
+        ref = O.preds_1d(prob, params, Xte)
+        crit_ref = O.criterion_1d(prob, params)
+    else:
+        prob, params, (Xte, ute), fs = problem_2d(n1=48, n2=40, Q=8, seed=7)
+        s = device_solver(prob, 8, fs)
+        s.set_params(params)
+        pred = s.predict(Xte[0], Xte[1])
+        ref = O.preds_2d(prob, params, Xte[0], Xte[1])
+        crit_ref = O.criterion_2d(prob, params)
+    assert rel(pred, ref) < 1e-10
+    assert abs(s.criterion() - crit_ref) / abs(crit_ref) < 1e-10
+    s.close()
+
+
+def test_step_deterministic():
+    prob, params, _, fs = problem_2d(n1=64, n2=64, Q=10, seed=8)
+    out = []
+    for _ in range(2):
+        s = device_solver(prob, 10, fs)
+        s.set_params(params)
+        s.step(3)
+        out.append(s.get_flat())
+        s.close()
+    assert np.array_equal(out[0], out[1])
