@@ -7,21 +7,24 @@
 // with closed-form fields instead of nested jax.grad.
 //
 // Design: d = |x_i - x_j| is exactly symmetric, so K and DD are bitwise symmetric and D_x1
-// bitwise antisymmetric.  One workgroup computes a 32x32 tile of the LOWER tile triangle and
-// writes it twice (direct + LDS-transposed mirror): half the exp/sincos work of a full
-// sweep.  Every thread evaluates 4 elements x Q components; per-axis constants (w, a, 2*pi*f)
+// bitwise antisymmetric.  Only the LOWER tile triangle is evaluated and every element is
+// written twice (direct + mirror): half the exp/sincos work of a full sweep.  The Q mixture
+// components of one element are spread over 4 waves (latency: a 256x256 factor pair is
+// ~1150 workgroups) and summed in fixed order through LDS; per-axis constants (w, a, 2*pi*f)
 // sit in LDS.  Pads (i or j >= n) are written as identity (K) / zero (D) so the padded SPD
 // inverse stays block-diagonal.
 #include "gpk_internal.h"
 
 namespace gpk {
 
+// Partial sums over components c = c0, c0 + cs, ... (cs = stride) of K and D at one pair.
 template <bool MATERN, bool COS, int DERIV>
-__device__ __forceinline__ void eval_kd(double diff, const double* w, const double* a,
-                                        const double* om, int q, double& K, double& D) {
+__device__ __forceinline__ void eval_kd_part(double diff, const double* w, const double* a,
+                                             const double* om, int c0, int cs, int q, double& K,
+                                             double& D) {
   double d = fabs(diff);
   double k = 0.0, dv = 0.0;
-  for (int c = 0; c < q; ++c) {
+  for (int c = c0; c < q; c += cs) {
     double m0, m1, m2;
     radial<MATERN>(d, a[c], m0, m1, m2);
     if (COS) {
@@ -38,8 +41,15 @@ __device__ __forceinline__ void eval_kd(double diff, const double* w, const doub
     }
   }
   K = k;
+  D = dv;  // unsigned: the D_x1 sign s_ij is applied by the caller
+}
+
+template <bool MATERN, bool COS, int DERIV>
+__device__ __forceinline__ void eval_kd(double diff, const double* w, const double* a,
+                                        const double* om, int q, double& K, double& D) {
+  eval_kd_part<MATERN, COS, DERIV>(diff, w, a, om, 0, 1, q, K, D);
   // JAX abs JVP: select(x >= 0, g, -g) -> sign(0) = +1
-  D = (DERIV == 1) ? (diff >= 0.0 ? dv : -dv) : dv;
+  if (DERIV == 1 && !(diff >= 0.0)) D = -D;
 }
 
 struct AssembleBatch {
@@ -47,20 +57,25 @@ struct AssembleBatch {
   int tiles[2];   // lower-triangle tile count per axis
 };
 
+constexpr int ASM_SUB = 16;  // workgroups per 32x32 tile: 64 elements (2 rows) each
+
+// grid.x = lower-triangle tile * 16 + sub-block, grid.y = axis.  Thread t: element
+// e = t&63 of the sub-block (row 2*sub + (e>>5), col e&31), component group g = t>>6
+// (components g, g+4, ...).  The 4 partial sums are added in fixed order through LDS and
+// wave 0 writes the element and its mirror (K symmetric, DD symmetric, D_x1 antisymmetric).
 template <bool MATERN, bool COS, int DERIV>
 __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
   const int axis = blockIdx.y;
   const AssembleArgs& A = b.ax[axis];
-  int tile = blockIdx.x;
+  const int tile = blockIdx.x / ASM_SUB, sub = blockIdx.x % ASM_SUB;
   if (tile >= b.tiles[axis]) return;
-  // lower-triangle tile index -> (I, J), I >= J
   int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
   while ((I + 1) * (I + 2) / 2 <= tile) ++I;
   while (I * (I + 1) / 2 > tile) --I;
-  int J = tile - I * (I + 1) / 2;
+  const int J = tile - I * (I + 1) / 2;
 
   __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
-  __shared__ double tK[32][33], tD[32][33];
+  __shared__ double pk[4][64], pd[4][64];
   const int t = threadIdx.x;
   if (t < q) {
     sw[t] = A.kc->w[t];
@@ -68,36 +83,35 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
     so[t] = A.kc->om[t];
   }
   __syncthreads();
-  const int tx = t & 31, ty = t >> 5;
-  const int j = J * 32 + tx;
-  const double xj = j < A.n ? A.x[j] : 0.0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int li = ty + 8 * r;
-    const int i = I * 32 + li;
-    double kv, dv;
-    if (i < A.n && j < A.n) {
-      eval_kd<MATERN, COS, DERIV>(A.x[i] - xj, sw, sa, so, q, kv, dv);
-      if (i == j) kv += A.jitter;
-    } else {
-      kv = (i == j) ? 1.0 : 0.0;
-      dv = 0.0;
-    }
-    A.K[(size_t)i * A.p + j] = kv;
-    if (DERIV) A.D[(size_t)i * A.p + j] = dv;
-    tK[li][tx] = kv;
-    tD[li][tx] = dv;
+  const int e = t & 63, g = t >> 6;
+  const int i = I * 32 + 2 * sub + (e >> 5), j = J * 32 + (e & 31);
+  const bool real = i < A.n && j < A.n;
+  double diff = 0.0, kv = 0.0, dv = 0.0;
+  if (real) {
+    diff = A.x[i] - A.x[j];
+    eval_kd_part<MATERN, COS, DERIV>(diff, sw, sa, so, g, 4, q, kv, dv);
   }
-  if (I == J) return;  // block-uniform
+  pk[g][e] = kv;
+  pd[g][e] = dv;
   __syncthreads();
-  // mirror tile (J, I): element (J*32+row, I*32+col) = tile(I,J)[col][row]
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = ty + 8 * r;
-    const size_t o = (size_t)(J * 32 + row) * A.p + I * 32 + tx;
-    A.K[o] = tK[tx][row];
-    if (DERIV == 2) A.D[o] = tD[tx][row];
-    if (DERIV == 1) A.D[o] = -tD[tx][row];  // D_x1 is antisymmetric (pads are 0 either way)
+  if (g != 0) return;
+  if (real) {
+    kv = (pk[0][e] + pk[1][e]) + (pk[2][e] + pk[3][e]);
+    dv = (pd[0][e] + pd[1][e]) + (pd[2][e] + pd[3][e]);
+    if (i == j) kv += A.jitter;
+  } else {
+    kv = (i == j) ? 1.0 : 0.0;  // padded block is the identity
+    dv = 0.0;
+  }
+  const double s_ij = (diff >= 0.0) ? 1.0 : -1.0;         // JAX abs'(0) = +1
+  const double s_ji = (-diff >= 0.0) ? 1.0 : -1.0;
+  A.K[(size_t)i * A.p + j] = kv;
+  if (DERIV == 2) A.D[(size_t)i * A.p + j] = dv;
+  if (DERIV == 1) A.D[(size_t)i * A.p + j] = real ? s_ij * dv : 0.0;
+  if (I != J) {
+    A.K[(size_t)j * A.p + i] = kv;
+    if (DERIV == 2) A.D[(size_t)j * A.p + i] = dv;
+    if (DERIV == 1) A.D[(size_t)j * A.p + i] = real ? s_ji * dv : 0.0;
   }
 }
 
@@ -128,7 +142,7 @@ __global__ __launch_bounds__(256) void cross_kernel(const double* __restrict__ x
 template <bool MATERN, bool COS>
 static void launch_assemble_t(const AssembleBatch& b, int naxes, int maxt, int q, int deriv,
                               hipStream_t s) {
-  dim3 grid(maxt, naxes);
+  dim3 grid(maxt * ASM_SUB, naxes);
   if (deriv == 2)
     hipLaunchKernelGGL((assemble_kernel<MATERN, COS, 2>), grid, dim3(256), 0, s, b, q);
   else if (deriv == 1)

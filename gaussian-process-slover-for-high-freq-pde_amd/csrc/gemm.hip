@@ -124,9 +124,129 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Latency-oriented variant for small factors (N <= ~512, e.g. the 256^2 headline): one
+// 16x16 output tile per workgroup so a 256x256 product fills 256 CUs; the K range (of each
+// product) is split over the 4 waves; operands go straight from L2 into registers, 8
+// k-substeps of loads in flight per wave; the 4 partial accumulators are summed through LDS
+// in fixed order (deterministic) by wave 0, which runs the epilogue.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ d4 mma_chunk(const double* __restrict__ A, int lda, int ta,
+                                        const double* __restrict__ B, int ldb, int tb, int i0,
+                                        int j0, int kbeg, int kend, int lane, d4 acc) {
+  const int li = lane & 15, lk = lane >> 4;
+  const int i = i0 + li, j = j0 + li;
+  int k0 = kbeg;
+  // 64-deep blocks: all 16 k-substeps of operands in flight before the first MFMA
+  for (; k0 + 64 <= kend; k0 += 64) {
+    double a[16], b[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = k0 + 4 * s + lk;
+      a[s] = ta ? A[(size_t)k * lda + i] : A[(size_t)i * lda + k];
+      b[s] = tb ? B[(size_t)j * ldb + k] : B[(size_t)k * ldb + j];
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+  }
+  if (k0 < kend) {  // K ranges are multiples of 32: at most one 32-deep tail
+    double a[8], b[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = k0 + 4 * s + lk;
+      a[s] = ta ? A[(size_t)k * lda + i] : A[(size_t)i * lda + k];
+      b[s] = tb ? B[(size_t)j * ldb + k] : B[(size_t)k * ldb + j];
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void gemm_small_kernel(const GemmDesc* __restrict__ descs,
+                                                         const StepScalars* __restrict__ sc) {
+  const GemmDesc& d = descs[blockIdx.y];
+  const int tn = d.N >> 4;
+  const int tiles = (d.M >> 4) * tn;
+  if ((int)blockIdx.x >= tiles) return;
+  const int i0 = (blockIdx.x / tn) * 16, j0 = (blockIdx.x % tn) * 16;
+  __shared__ double part[2][4][256];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // K ranges are multiples of 32; wave wv takes a contiguous quarter (rounded to 32)
+  auto range = [&](int K, int& b0, int& b1) {
+    const int nk = K >> 5;
+    b0 = ((nk * wv) >> 2) << 5;
+    b1 = ((nk * (wv + 1)) >> 2) << 5;
+  };
+  // wave 0 runs the epilogue: prefetch its operands now so their latency hides under the MFMAs
+  double pre[4] = {0.0, 0.0, 0.0, 0.0}, pu[4] = {0.0, 0.0, 0.0, 0.0};
+  if (wv == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = i0 + (lane >> 4) + 4 * r, col = j0 + (lane & 15);
+      if ((d.epi == EPI_STORE && d.beta != 0.0) || d.epi == EPI_HALFS)
+        pre[r] = d.C0[(size_t)row * d.ldc0 + col];
+      else if (d.epi == EPI_RESID)
+        pre[r] = d.F[(size_t)row * d.ldf + col];
+      if (d.epi == EPI_QUAD || (d.epi == EPI_RESID && d.ac)) pu[r] = d.U[(size_t)row * d.ldf + col];
+    }
+  }
+  int b0, b1;
+  range(d.K, b0, b1);
+  d4 acc1 = {0.0, 0.0, 0.0, 0.0}, acc2 = {0.0, 0.0, 0.0, 0.0};
+  acc1 = mma_chunk(d.A, d.lda, d.ta, d.B, d.ldb, d.tb, i0, j0, b0, b1, lane, acc1);
+  if (d.K2) {
+    range(d.K2, b0, b1);
+    acc2 = mma_chunk(d.A2, d.lda2, d.ta2, d.B2, d.ldb2, d.tb2, i0, j0, b0, b1, lane, acc2);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    part[0][wv][lane * 4 + r] = acc1[r];
+    part[1][wv][lane * 4 + r] = acc2[r];
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  double alpha = d.alpha;
+  if (d.vscale) alpha *= sc->v;
+  double red = 0.0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int q = lane * 4 + r;
+    const double s1 = (part[0][0][q] + part[0][1][q]) + (part[0][2][q] + part[0][3][q]);
+    const int row = i0 + (lane >> 4) + 4 * r, col = j0 + (lane & 15);
+    double c = alpha * s1;
+    if (d.K2) c += d.alpha2 * ((part[1][0][q] + part[1][1][q]) + (part[1][2][q] + part[1][3][q]));
+    switch (d.epi) {
+      case EPI_STORE:
+        if (d.beta != 0.0) c += d.beta * pre[r];
+        break;
+      case EPI_RESID:
+        c -= pre[r];
+        if (d.ac) c += pu[r] * (pu[r] * pu[r] - 1.0);
+        red += c * c;
+        break;
+      case EPI_QUAD:
+        red += c * pu[r];
+        break;
+      case EPI_HALFS:
+        c += 0.5 * pre[r];
+        break;
+    }
+    d.C[(size_t)row * d.ldc + col] = c;
+  }
+  if (d.red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) red += __shfl_xor(red, o, 64);
+    if (lane == 0) d.red[blockIdx.x] = red;
+  }
+}
+
 hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles,
-                             const StepScalars* sc, hipStream_t s) {
-  hipLaunchKernelGGL(gemm_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, descs_dev, sc);
+                             const StepScalars* sc, hipStream_t s, int small) {
+  if (small)
+    hipLaunchKernelGGL(gemm_small_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, descs_dev, sc);
+  else
+    hipLaunchKernelGGL(gemm_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, descs_dev, sc);
   return hipGetLastError();
 }
 

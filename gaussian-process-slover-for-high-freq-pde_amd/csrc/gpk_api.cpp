@@ -57,7 +57,7 @@ struct DevSwitch {  // restore the caller's current device on scope exit
 };
 
 struct Stage {
-  int off = 0, n = 0, maxtiles = 0;
+  int off = 0, n = 0, maxtiles = 0, small = 0;
 };
 
 }  // namespace
@@ -178,7 +178,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
   if (L.dim == 2) {
     for (int k = 0; k < 5; ++k) {
       TRY(check_launch(launch_gemm_batch(h->descs + h->st[k].off, h->st[k].n, h->st[k].maxtiles,
-                                         h->sc, h->s), "gemm"));
+                                         h->sc, h->s, h->st[k].small), "gemm"));
       mark(h, stage++);
     }
     PGradArgs pa[2];
@@ -263,9 +263,15 @@ static int build_descs(gpk_handle* h) {
   auto begin = [&](int k) { h->st[k].off = (int)d.size(); };
   auto end = [&](int k) {
     h->st[k].n = (int)d.size() - h->st[k].off;
-    int mt = 0;
-    for (int i = h->st[k].off; i < (int)d.size(); ++i) mt = std::max(mt, (d[i].M / 32) * (d[i].N / 32));
-    h->st[k].maxtiles = mt;
+    int mt32 = 0, mt16 = 0;
+    long tot16 = 0;
+    for (int i = h->st[k].off; i < (int)d.size(); ++i) {
+      mt32 = std::max(mt32, (d[i].M / 32) * (d[i].N / 32));
+      mt16 = std::max(mt16, (d[i].M / 16) * (d[i].N / 16));
+      tot16 += (long)(d[i].M / 16) * (d[i].N / 16);
+    }
+    h->st[k].small = gemm_use_small(tot16) ? 1 : 0;
+    h->st[k].maxtiles = h->st[k].small ? mt16 : mt32;
   };
   // Stage A: A = K1^{-1} U, Bt = U K2^{-1}        (model_GP_solver_2d.py:104-105)
   begin(0);
@@ -286,6 +292,7 @@ static int build_descs(gpk_handle* h) {
     d.push_back(r);
   }
   end(1);
+  h->nquad = h->negap = h->st[1].small ? (P1 / 16) * (P2 / 16) : (P1 / 32) * (P2 / 32);
   // Stage C: T1 = D1^T R, T2 = R D2, G_D1 = v beta R A^T, G_D2 = v R^T Bt   (Appendix A)
   begin(2);
   d.push_back(mk(h->D[0], P1, 1, h->R, P2, 0, h->T1, P2, P1, P2, P1));
@@ -549,7 +556,7 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
       A_(h->GK[a], (size_t)P * P);
       A_(h->GD[a], (size_t)P * P);
     }
-    h->nquad = h->negap = (P1 / 32) * (P2 / 32);
+    h->nquad = h->negap = (P1 / 16) * (P2 / 16);  // upper bound (16x16 tiles); set in build_descs
   } else {
     A_(h->alpha, P1); A_(h->R, P1); A_(h->tvec, P1); A_(h->beta, P1);
     h->nquad = h->negap = gemv_blocks(P1);
@@ -762,8 +769,11 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
     if (hipMalloc(&dd, sizeof(d)) != hipSuccess) { cleanup(); return fail(GPK_ENOMEM, "hipMalloc"); }
     tmp.push_back(dd);
     (void)hipMemcpyAsync(dd, d, sizeof(d), hipMemcpyHostToDevice, h->s);
-    for (int k = 0; k < 4; ++k)
-      (void)launch_gemm_batch(dd + k, 1, (d[k].M / 32) * (d[k].N / 32), h->sc, h->s);
+    for (int k = 0; k < 4; ++k) {
+      const long t16 = (long)(d[k].M / 16) * (d[k].N / 16);
+      const int small = gemm_use_small(t16) ? 1 : 0;
+      (void)launch_gemm_batch(dd + k, 1, small ? (int)t16 : (d[k].M / 32) * (d[k].N / 32), h->sc, h->s, small);
+    }
     for (int i = 0; i < m1; ++i)
       (void)hipMemcpyAsync(out + (size_t)i * m2, res + (size_t)i * M2p, m2 * sizeof(double),
                            hipMemcpyDeviceToHost, h->s);

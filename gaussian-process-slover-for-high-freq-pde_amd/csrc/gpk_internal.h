@@ -129,8 +129,11 @@ struct GemmDesc {
   int vscale;               // multiply alpha by v (StepScalars) when 1
   double* red;              // per-tile partial sums, [tiles] (nullable)
 };
+// small = 1: 16x16-tile latency kernel (max_tiles counts 16x16 tiles); 0: 32x32 LDS-tiled
 hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles,
-                             const StepScalars* sc, hipStream_t s);
+                             const StepScalars* sc, hipStream_t s, int small);
+// heuristic: use the 16x16 latency kernel while the whole stage has few enough tiles
+inline bool gemm_use_small(long tiles16_total) { return tiles16_total <= 16384; }
 
 // GEMV y = alpha * A x (A padded p x p, op N), optional epilogues like GEMM
 struct GemvDesc {

@@ -8,9 +8,9 @@
 //
 // The fields depend on d = |x_i - x_j| only, so each unordered pair is evaluated once with
 // its mirror's weight folded in (D_x1's sign s_ij folded into the weight).  A workgroup
-// stages 256 pairs (d, w_K, w_D) in LDS; thread (g = t>>5, q = t&31) walks every 8th pair for
+// stages 64 pairs (d, w_K, w_D) in LDS; thread (g = t>>5, q = t&31) walks every 8th pair for
 // mixture component q, so each (pair, q) costs one exp + one sincos; 8-way LDS reduction at
-// the end leaves 3*Q deterministic partials per workgroup.
+// the end leaves 3*Q deterministic partials per workgroup (~1150 workgroups at N = 256).
 //
 // 2D mode reads materialised G_K / G_D tiles; 1D mode forms them on the fly from K^{-1} and
 // the vectors alpha = K^{-1}u, beta = K^{-1}D^T R, R (model_GP_solver_1d.py:80-149):
@@ -19,7 +19,8 @@
 
 namespace gpk {
 
-constexpr int PAIRS = 256;  // pairs per workgroup = 8 rows x 32 cols of a 32x32 tile
+constexpr int PAIRS = 64;   // pairs per workgroup = 2 rows x 32 cols of a 32x32 tile
+constexpr int PG_SUB = 1024 / PAIRS;  // workgroups per tile
 
 struct PGradBatch {
   PGradArgs ax[2];
@@ -32,7 +33,7 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
   const int axis = blockIdx.y;
   const PGradArgs& A = b.ax[axis];
   const int blk = blockIdx.x;
-  const int tile = blk >> 2, chunk = blk & 3;
+  const int tile = blk / PG_SUB, chunk = blk % PG_SUB;
   if (tile >= b.tiles[axis]) return;
   int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
   while ((I + 1) * (I + 2) / 2 <= tile) ++I;
@@ -48,8 +49,8 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
     sa[t] = A.kc->a[t];
     so[t] = A.kc->om[t];
   }
-  {  // stage pair t
-    const int i = I * 32 + chunk * 8 + (t >> 5), j = J * 32 + (t & 31);
+  if (t < PAIRS) {  // stage pair t
+    const int i = I * 32 + chunk * (PAIRS / 32) + (t >> 5), j = J * 32 + (t & 31);
     double d = 0.0, wk = 0.0, wd = 0.0;
     if (i < A.n && j < A.n) {
       const double diff = A.x[i] - A.x[j];
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
 
 int pgrad_blocks(int n) {
   int T = pad_up(n) / 32;
-  return T * (T + 1) / 2 * 4;
+  return T * (T + 1) / 2 * PG_SUB;
 }
 
 template <bool MATERN, bool COS>

@@ -6,7 +6,7 @@
 // becomes an MFMA GEMM against K^{-1} and the log-det falls out of the Cholesky pivots.
 //
 // Algorithm: blocked Cholesky-Gauss-Jordan sweep, 32x32 pivot blocks.  For pivot block P
-// (the current Schur complement S = X_PP = L L^T, factored in LDS):
+// (the current Schur complement S = X_PP = L L^T, Cholesky-factored in LDS by one workgroup):
 //     V   = L^{-1} X_P.                  (panel "TRSM" by MFMA against L^{-1})
 //     X_RR -= V_R^T V_R                  (symmetric rank-32 update, like SYRK)
 //     X_PR  = L^{-T} V_R,  X_RP = X_PR^T,  X_PP = -L^{-T} L^{-1}
@@ -31,41 +31,71 @@ constexpr int SA = 34;  // LDS row stride for A-role tiles (conflict-free ds_rea
 constexpr int SB = 48;  // LDS row stride for B-role tiles (conflict-free B[k][j])
 constexpr int SP = 33;  // pivot scratch stride
 
-// One wave: in-place Cholesky of the 32x32 SPD block A (lower part used) and L^{-1} into M.
-// Right-looking: step k scales column k of A and row k of M by 1/L_kk, then applies the
-// rank-1 elimination to the trailing A and to M's rows below k.  Returns sum_k log A_kk
-// (= 2 sum log L_kk = log det of the block).
-__device__ double pivot_chol_inv_wave(double* A, double* M, int lane, int* status) {
-  for (int e = lane; e < 1024; e += 64) M[(e >> 5) * SP + (e & 31)] = ((e >> 5) == (e & 31)) ? 1.0 : 0.0;
-  double ls = 0.0;
-  const int col = lane & 31, r0 = lane >> 5;
-  for (int k = 0; k < 32; ++k) {
-    const double p = A[k * SP + k];
-    if (!(p > 0.0)) {
-      if (lane == 0) atomicOr(status, 1);
-    }
-    ls += log(p);
-    const double r = 1.0 / sqrt(p);
-    // phase 1: l_ik = A[i][k] * r (i > k), L_kk = sqrt(p); M[k][c] *= r (c <= k)
-    if (lane < 32) {
-      const int i = lane;
-      if (i > k) A[i * SP + k] = A[i * SP + k] * r;
-      if (i == k) A[k * SP + k] = p * r;
-    } else {
-      const int c = lane - 32;
-      if (c <= k) M[k * SP + c] = M[k * SP + c] * r;
-    }
-    // phase 2: trailing A[i][j] -= l_ik l_jk (i >= j > k); M[i][c] -= l_ik M[k][c] (i > k, c <= k)
+// One workgroup (256 threads): Cholesky of the 32x32 SPD block A = L L^T (LDS, stride SP,
+// full symmetric storage) and M = L^{-1} (LDS, stride SP).  Thread t owns column c = t&31,
+// rows i = (t>>5) + 8r (r = 0..3) of both.  Right-looking step k:
+//   p = A[k][k], rs = 1/sqrt(p);  l_ic = A[k][i] rs (row k = column k by symmetry)
+//   A[i][c] -= l_ik l_ck  (i, c > k)          M[i][c] -= l_ik (rs M[k][c])  (i > k)
+// Row k of M is scaled by rs lazily (after the loop), so step k writes only rows > k and one
+// barrier per step orders everything.  The serial chain per step is one LDS read, v_rsq_f64
+// + two Newton steps (no fp64 sqrt/div sequences), a few FMAs, the barrier; the log det
+// (sum_k log p_k) is formed after the loop, one log per lane.  Returns it in thread 0.
+__device__ __forceinline__ double rsqrt_f64(double p) {
+  double y = __builtin_amdgcn_rsq(p);          // ~2^-29 relative
+  double e = fma(-p * y, y, 1.0);              // 1 - p y^2
+  y = fma(0.5 * y, e, y);
+  e = fma(-p * y, y, 1.0);
+  return fma(0.5 * y, e, y);
+}
+
+__device__ __forceinline__ double pivot_chol_inv_block(double* A, double* M, double* pv, int t,
+                                                       int* status) {
+  const int c = t & 31, i0 = t >> 5;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const int i = r0 + 2 * m, j = col;
-      const double lik = A[i * SP + k];
-      if (i > k) {
-        if (j > k && j <= i) A[i * SP + j] -= lik * A[j * SP + k];
-        if (j <= k) M[i * SP + j] -= lik * M[k * SP + j];
-      }
+  for (int r = 0; r < 4; ++r) M[(i0 + 8 * r) * SP + c] = (i0 + 8 * r == c) ? 1.0 : 0.0;
+  __syncthreads();
+  for (int k = 0; k < 32; ++k) {
+    // all LDS reads of the step first (one wait), then branch-free math, then the writes;
+    // rows <= k are rewritten with their unchanged value (benign: same bits)
+    const double p = A[k * SP + k];
+    const double akc = A[k * SP + c], mkc0 = M[k * SP + c];
+    double aki[4], aic[4], mic[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 8 * r;
+      aki[r] = A[k * SP + i];
+      aic[r] = A[i * SP + c];
+      mic[r] = M[i * SP + c];
     }
+    const double rs = rsqrt_f64(p);
+    if (t == 0) pv[k] = p;
+    const double lck = akc * rs, mkc = mkc0 * rs;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 8 * r;
+      const double lik = aki[r] * rs;
+      const double na = (i > k && c > k) ? fma(-lik, lck, aic[r]) : aic[r];
+      const double nm = (i > k) ? fma(-lik, mkc, mic[r]) : mic[r];
+      A[i * SP + c] = na;
+      M[i * SP + c] = nm;
+    }
+    __syncthreads();
   }
+  // lazy row scaling of L^{-1}; log det from the 32 pivots
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 8 * r;
+    M[i * SP + c] *= rsqrt_f64(pv[i]);
+  }
+  double ls = 0.0;
+  if (t < 64) {
+    const double pk = pv[t & 31];
+    if (t < 32 && !(pk > 0.0)) atomicOr(status, 1);
+    ls = (t < 32) ? log(pk) : 0.0;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+  }
+  __syncthreads();
   return ls;
 }
 
@@ -79,19 +109,18 @@ struct SpdBatch {
   int* status[2];
 };
 
-__global__ __launch_bounds__(64) void pivot_init_kernel(SpdBatch b) {
+__global__ __launch_bounds__(256) void pivot_init_kernel(SpdBatch b) {
   const int m = blockIdx.x;
-  __shared__ double A[32 * SP], M[32 * SP];
-  const int lane = threadIdx.x;
+  __shared__ double A[32 * SP], M[32 * SP], pv[32];
+  const int t = threadIdx.x;
   const double* X = b.X[m];
   const int p = b.p[m];
-  for (int e = lane; e < 1024; e += 64) A[(e >> 5) * SP + (e & 31)] = X[(size_t)(e >> 5) * p + (e & 31)];
+  for (int e = t; e < 1024; e += 256) A[(e >> 5) * SP + (e & 31)] = X[(size_t)(e >> 5) * p + (e & 31)];
   __syncthreads();
-  const double ls = pivot_chol_inv_wave(A, M, lane, b.status[m]);
-  __syncthreads();
+  const double ls = pivot_chol_inv_block(A, M, pv, t, b.status[m]);
   double* piv = b.piv[m];
-  for (int e = lane; e < 1024; e += 64) piv[e] = M[(e >> 5) * SP + (e & 31)];
-  if (lane == 0) b.ldet[m][0] = ls;
+  for (int e = t; e < 1024; e += 256) piv[e] = M[(e >> 5) * SP + (e & 31)];
+  if (t == 0) b.ldet[m][0] = ls;
 }
 
 // acc += A(32x32, element (i,k) at a[i*sai + k*sak]) * B(32x32, (k,j) at bm[k*sbk + j*sbj]),
@@ -129,12 +158,19 @@ __global__ __launch_bounds__(256) void sweep_kernel(SpdBatch b, int k) {
 
   __shared__ double sL[32 * SA];                 // L^{-1}
   __shared__ double sXI[32 * SB], sXJ[32 * SB];  // X_PI, X_PJ, then V_I, V_J
-  __shared__ double sP[32 * SP], sM[32 * SP];    // next-pivot scratch
+  __shared__ double sP[32 * SP], sM[32 * SP], pv[32];  // next-pivot scratch
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int tx = t & 31, ty = t >> 5;
   const int P = k;
 
+  // prefetch this wave's quadrant of X_IJ (consumed only in the epilogue)
+  double xij[4] = {0.0, 0.0, 0.0, 0.0};
+  if (I != P && J != P) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      xij[r] = X[(size_t)(I * 32 + 16 * wr + (lane >> 4) + 4 * r) * p + J * 32 + 16 * wc + (lane & 15)];
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = ty + 8 * r;
@@ -176,18 +212,16 @@ __global__ __launch_bounds__(256) void sweep_kernel(SpdBatch b, int k) {
     else if (I == P || J == P)
       y = acc[r];
     else
-      y = X[o] - acc[r];
+      y = xij[r] - acc[r];
     Y[o] = y * fin;
     if (nextpiv) sP[row * SP + col] = y;
   }
   if (!nextpiv) return;  // block-uniform
   __syncthreads();
-  if (wv == 0) {
-    const double ls = pivot_chol_inv_wave(sP, sM, lane, b.status[m]);
-    double* piv = b.piv[m] + (size_t)(k + 1) * 1024;
-    for (int e = lane; e < 1024; e += 64) piv[e] = sM[(e >> 5) * SP + (e & 31)];
-    if (lane == 0) b.ldet[m][k + 1] = ls;
-  }
+  const double ls = pivot_chol_inv_block(sP, sM, pv, t, b.status[m]);
+  double* piv = b.piv[m] + (size_t)(k + 1) * 1024;
+  for (int e = t; e < 1024; e += 256) piv[e] = sM[(e >> 5) * SP + (e & 31)];
+  if (t == 0) b.ldet[m][k + 1] = ls;
 }
 
 hipError_t launch_spd_inverse(SpdArgs* a, int nmat, double** final_out, hipStream_t s) {
@@ -205,7 +239,7 @@ hipError_t launch_spd_inverse(SpdArgs* a, int nmat, double** final_out, hipStrea
     // sweep k reads (k even ? X : Y) and writes the other; T sweeps end in:
     final_out[m] = (b.T[m] & 1) ? a[m].Y : a[m].X;
   }
-  hipLaunchKernelGGL(pivot_init_kernel, dim3(nmat), dim3(64), 0, s, b);
+  hipLaunchKernelGGL(pivot_init_kernel, dim3(nmat), dim3(256), 0, s, b);
   for (int k = 0; k < Tmax; ++k)
     hipLaunchKernelGGL(sweep_kernel, dim3(Tmax * Tmax, nmat), dim3(256), 0, s, b, k);
   return hipGetLastError();

@@ -134,6 +134,14 @@ const char* gpk_stage_name(const gpk_handle* h, int32_t stage);
  * `iters` times on the handle's stream; returns average microseconds per call. */
 int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us);
 
+/* One kernel of the step, launched `iters` times back to back on the handle's stream
+ * between two HIP events (after one full step so its inputs are valid; every listed kernel
+ * is idempotent).  name: "assemble" | "sweep" | "gemm_B" | "pgrad".  Returns the average
+ * device time per launch and the kernel's ALGORITHMIC work per launch (flops, HBM bytes;
+ * DESIGN.md §Measurement defines them). */
+int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg_us,
+                     double* alg_flops, double* alg_bytes);
+
 #ifdef __cplusplus
 }
 #endif
