@@ -106,10 +106,12 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
   const double s_ij = (diff >= 0.0) ? 1.0 : -1.0;         // JAX abs'(0) = +1
   const double s_ji = (-diff >= 0.0) ? 1.0 : -1.0;
   A.K[(size_t)i * A.p + j] = kv;
+  if (A.Kc) A.Kc[(size_t)i * A.p + j] = kv;
   if (DERIV == 2) A.D[(size_t)i * A.p + j] = dv;
   if (DERIV == 1) A.D[(size_t)i * A.p + j] = real ? s_ij * dv : 0.0;
   if (I != J) {
     A.K[(size_t)j * A.p + i] = kv;
+    if (A.Kc) A.Kc[(size_t)j * A.p + i] = kv;
     if (DERIV == 2) A.D[(size_t)j * A.p + i] = dv;
     if (DERIV == 1) A.D[(size_t)j * A.p + i] = real ? s_ji * dv : 0.0;
   }
@@ -137,6 +139,49 @@ __global__ __launch_bounds__(256) void cross_kernel(const double* __restrict__ x
   if (i == j) kv += jitter;
   K[(size_t)i * ld + j] = kv;
   if (DERIV) D[(size_t)i * ld + j] = dv;
+}
+
+// elementwise pairs: out[e] = kappa / D_x1 / DD_x1 at (x1[e], x2[e]) -- vmap(kappa) semantics
+template <bool MATERN, bool COS, int DERIV>
+__global__ __launch_bounds__(256) void pairs_kernel(const double* __restrict__ x1,
+                                                    const double* __restrict__ x2, long n,
+                                                    const AxisConst* kc, int q, double* out) {
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
+  const int t = threadIdx.x;
+  if (t < q) {
+    sw[t] = kc->w[t];
+    sa[t] = kc->a[t];
+    so[t] = kc->om[t];
+  }
+  __syncthreads();
+  const long e = (long)blockIdx.x * 256 + t;
+  if (e >= n) return;
+  double kv, dv;
+  eval_kd<MATERN, COS, DERIV>(x1[e] - x2[e], sw, sa, so, q, kv, dv);
+  out[e] = DERIV ? dv : kv;
+}
+
+template <bool MATERN, bool COS>
+static void launch_pairs_t(const double* x1, const double* x2, long n, const AxisConst* kc, int q,
+                           int deriv, double* out, hipStream_t s) {
+  dim3 grid((unsigned)((n + 255) / 256));
+  if (deriv == 2)
+    hipLaunchKernelGGL((pairs_kernel<MATERN, COS, 2>), grid, dim3(256), 0, s, x1, x2, n, kc, q, out);
+  else if (deriv == 1)
+    hipLaunchKernelGGL((pairs_kernel<MATERN, COS, 1>), grid, dim3(256), 0, s, x1, x2, n, kc, q, out);
+  else
+    hipLaunchKernelGGL((pairs_kernel<MATERN, COS, 0>), grid, dim3(256), 0, s, x1, x2, n, kc, q, out);
+}
+
+hipError_t launch_pairs(int kind, int q, const double* x1, const double* x2, long n,
+                        const AxisConst* kc, int deriv, double* out, hipStream_t s) {
+  switch (kind) {
+    case SE_COS: launch_pairs_t<false, true>(x1, x2, n, kc, q, deriv, out, s); break;
+    case MATERN52_COS: launch_pairs_t<true, true>(x1, x2, n, kc, q, deriv, out, s); break;
+    case SE: launch_pairs_t<false, false>(x1, x2, n, kc, q, deriv, out, s); break;
+    default: launch_pairs_t<true, false>(x1, x2, n, kc, q, deriv, out, s); break;
+  }
+  return hipGetLastError();
 }
 
 template <bool MATERN, bool COS>

@@ -58,20 +58,63 @@ __device__ __forceinline__ double block_sum_256(double v, double* red) {
   return s;
 }
 
+// Epilogue operands of one output element, fetched early (their latency hides under MFMA).
+struct EpiIn {
+  double pre, pu, q12;
+};
+
+__device__ __forceinline__ EpiIn epi_fetch(const GemmDesc& d, int row, int col) {
+  EpiIn e{0.0, 0.0, 0.0};
+  const size_t fo = (size_t)row * d.ldf + col;
+  if ((d.epi == EPI_STORE || d.epi == EPI_QUAD) && d.beta != 0.0)
+    e.pre = d.C0[(size_t)row * d.ldc0 + col];
+  else if (d.epi == EPI_RESID)
+    e.pre = d.F[fo];
+  if (d.epi == EPI_QUAD || (d.epi == EPI_RESID && d.ac)) e.pu = d.U[fo];
+  if (d.epi == EPI_RESID && d.red2) e.q12 = d.Q1[fo] * d.Q2[fo];
+  return e;
+}
+
+// c = alpha*P1 + alpha2*P2 (already formed); returns the stored value, accumulates partials
+__device__ __forceinline__ double epi_apply(const GemmDesc& d, double c, const EpiIn& e,
+                                            double& part, double& part2) {
+  switch (d.epi) {
+    case EPI_STORE:
+      if (d.beta != 0.0) c += d.beta * e.pre;
+      break;
+    case EPI_RESID:
+      c -= e.pre;
+      if (d.ac) c += e.pu * (e.pu * e.pu - 1.0);
+      part += c * c;
+      part2 += e.q12;
+      break;
+    case EPI_QUAD:
+      if (d.beta != 0.0) c += d.beta * e.pre;
+      part += c * e.pu;
+      break;
+  }
+  return c;
+}
+
 __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc* __restrict__ descs,
                                                    const StepScalars* __restrict__ sc) {
   const GemmDesc& d = descs[blockIdx.y];
   const int tn = d.N >> 5;
   const int tiles = (d.M >> 5) * tn;
   if ((int)blockIdx.x >= tiles) return;
+  if (!refine_gate_open(d.gate, d.ngate)) return;  // refinement not needed (uniform)
   const int ti = blockIdx.x / tn, tj = blockIdx.x % tn;
   const int i0 = ti * 32, j0 = tj * 32;
 
   __shared__ double sA[32 * GSA];
   __shared__ double sB[32 * GSB];
-  __shared__ double sred[4];
+  __shared__ double sred[4], sred2[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
+  EpiIn ein[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    ein[r] = epi_fetch(d, i0 + 16 * wr + (lane >> 4) + 4 * r, j0 + 16 * wc + (lane & 15));
 
   d4 acc1 = {0.0, 0.0, 0.0, 0.0}, acc2 = {0.0, 0.0, 0.0, 0.0};
   for (int k0 = 0; k0 < d.K; k0 += 32) {
@@ -87,40 +130,24 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc* __restrict__ 
     __syncthreads();
   }
 
-  double alpha = d.alpha;
+  double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
-  double part = 0.0;
+  if (d.vscale2) alpha2 *= sc->v;
+  double part = 0.0, part2 = 0.0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = i0 + 16 * wr + (lane >> 4) + 4 * r, col = j0 + 16 * wc + (lane & 15);
     double c = alpha * acc1[r];
-    if (d.K2) c += d.alpha2 * acc2[r];
-    switch (d.epi) {
-      case EPI_STORE:
-        if (d.beta != 0.0) c += d.beta * d.C0[(size_t)row * d.ldc0 + col];
-        break;
-      case EPI_RESID: {
-        const size_t fo = (size_t)row * d.ldf + col;
-        c -= d.F[fo];
-        if (d.ac) {
-          const double u = d.U[fo];
-          c += u * (u * u - 1.0);
-        }
-        part += c * c;
-        break;
-      }
-      case EPI_QUAD:
-        part += c * d.U[(size_t)row * d.ldf + col];
-        break;
-      case EPI_HALFS:
-        c += 0.5 * d.C0[(size_t)row * d.ldc0 + col];
-        break;
-    }
-    d.C[(size_t)row * d.ldc + col] = c;
+    if (d.K2) c += alpha2 * acc2[r];
+    d.C[(size_t)row * d.ldc + col] = epi_apply(d, c, ein[r], part, part2);
   }
   if (d.red) {
     double s = block_sum_256(part, sred);
     if (t == 0) d.red[blockIdx.x] = s;
+  }
+  if (d.red2) {
+    double s = block_sum_256(part2, sred2);
+    if (t == 0) d.red2[blockIdx.x] = s;
   }
 }
 
@@ -169,6 +196,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmDesc* __restr
   const int tn = d.N >> 4;
   const int tiles = (d.M >> 4) * tn;
   if ((int)blockIdx.x >= tiles) return;
+  if (!refine_gate_open(d.gate, d.ngate)) return;  // refinement not needed (uniform)
   const int i0 = (blockIdx.x / tn) * 16, j0 = (blockIdx.x % tn) * 16;
   __shared__ double part[2][4][256];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -179,17 +207,10 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmDesc* __restr
     b1 = ((nk * (wv + 1)) >> 2) << 5;
   };
   // wave 0 runs the epilogue: prefetch its operands now so their latency hides under the MFMAs
-  double pre[4] = {0.0, 0.0, 0.0, 0.0}, pu[4] = {0.0, 0.0, 0.0, 0.0};
+  EpiIn ein[4] = {};
   if (wv == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = i0 + (lane >> 4) + 4 * r, col = j0 + (lane & 15);
-      if ((d.epi == EPI_STORE && d.beta != 0.0) || d.epi == EPI_HALFS)
-        pre[r] = d.C0[(size_t)row * d.ldc0 + col];
-      else if (d.epi == EPI_RESID)
-        pre[r] = d.F[(size_t)row * d.ldf + col];
-      if (d.epi == EPI_QUAD || (d.epi == EPI_RESID && d.ac)) pu[r] = d.U[(size_t)row * d.ldf + col];
-    }
+    for (int r = 0; r < 4; ++r) ein[r] = epi_fetch(d, i0 + (lane >> 4) + 4 * r, j0 + (lane & 15));
   }
   int b0, b1;
   range(d.K, b0, b1);
@@ -206,38 +227,28 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmDesc* __restr
   }
   __syncthreads();
   if (wv != 0) return;
-  double alpha = d.alpha;
+  double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
-  double red = 0.0;
+  if (d.vscale2) alpha2 *= sc->v;
+  double red = 0.0, red2 = 0.0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int q = lane * 4 + r;
     const double s1 = (part[0][0][q] + part[0][1][q]) + (part[0][2][q] + part[0][3][q]);
     const int row = i0 + (lane >> 4) + 4 * r, col = j0 + (lane & 15);
     double c = alpha * s1;
-    if (d.K2) c += d.alpha2 * ((part[1][0][q] + part[1][1][q]) + (part[1][2][q] + part[1][3][q]));
-    switch (d.epi) {
-      case EPI_STORE:
-        if (d.beta != 0.0) c += d.beta * pre[r];
-        break;
-      case EPI_RESID:
-        c -= pre[r];
-        if (d.ac) c += pu[r] * (pu[r] * pu[r] - 1.0);
-        red += c * c;
-        break;
-      case EPI_QUAD:
-        red += c * pu[r];
-        break;
-      case EPI_HALFS:
-        c += 0.5 * pre[r];
-        break;
-    }
-    d.C[(size_t)row * d.ldc + col] = c;
+    if (d.K2) c += alpha2 * ((part[1][0][q] + part[1][1][q]) + (part[1][2][q] + part[1][3][q]));
+    d.C[(size_t)row * d.ldc + col] = epi_apply(d, c, ein[r], red, red2);
   }
   if (d.red) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) red += __shfl_xor(red, o, 64);
     if (lane == 0) d.red[blockIdx.x] = red;
+  }
+  if (d.red2) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) red2 += __shfl_xor(red2, o, 64);
+    if (lane == 0) d.red2[blockIdx.x] = red2;
   }
 }
 
@@ -254,7 +265,8 @@ hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles
 // GEMV (1D solver, code/model_GP_solver_1d.py:92,97): one wave per row, 4 rows per block.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void gemv_kernel(GemvDesc d) {
-  __shared__ double sred[4];
+  if (!refine_gate_open(d.gate, d.ngate)) return;  // refinement not needed (uniform)
+  __shared__ double sred[4], sred2[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int row = blockIdx.x * 4 + wv;
   double acc = 0.0;
@@ -264,9 +276,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvDesc d) {
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  double part = 0.0;
+  double part = 0.0, part2 = 0.0;
   if (lane == 0 && row < d.rows) {
     double y = d.alpha * acc;
+    if (d.beta != 0.0) y += d.beta * d.C0[row];
     if (d.epi == EPI_RESID) {
       y -= d.F[row];
       if (d.ac) {
@@ -277,12 +290,17 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvDesc d) {
     } else if (d.epi == EPI_QUAD) {
       part = y * d.U[row];
     }
+    if (d.red2) part2 = d.Q1[row] * d.Q2[row];
     d.y[row] = y;
   }
-  if (d.red) {
-    if (lane == 0) sred[wv] = part;
+  if (d.red || d.red2) {
+    if (lane == 0) {
+      sred[wv] = part;
+      sred2[wv] = part2;
+    }
     __syncthreads();
-    if (t == 0) d.red[blockIdx.x] = (sred[0] + sred[1]) + (sred[2] + sred[3]);
+    if (t == 0 && d.red) d.red[blockIdx.x] = (sred[0] + sred[1]) + (sred[2] + sred[3]);
+    if (t == 0 && d.red2) d.red2[blockIdx.x] = (sred2[0] + sred2[1]) + (sred2[2] + sred2[3]);
   }
 }
 

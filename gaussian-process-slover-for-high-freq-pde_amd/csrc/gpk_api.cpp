@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -39,11 +40,16 @@ static int fail(int code, const std::string& msg) {
 namespace {
 
 constexpr int LOSS_CAP = 4096;
-const char* kStageNames1D[] = {"prep", "assemble", "spd_inverse", "gemv_alpha", "gemv_resid",
-                               "gemv_DtR", "gemv_beta", "pgrad", "reduce", "finalize", "adam_u"};
-const char* kStageNames2D[] = {"prep", "assemble", "spd_inverse", "gemm_A", "gemm_B", "gemm_C",
-                               "gemm_D", "gemm_E", "pgrad", "reduce", "finalize", "adam_u"};
-constexpr int kMaxStages = 12;
+const char* kStageNames1D[] = {"prep", "assemble", "spd_inverse", "gemv_alpha", "gemv_alpha_res",
+                               "gemv_alpha_fix", "gemv_resid", "gemv_DtR", "gemv_beta",
+                               "gemv_beta_res", "gemv_beta_fix", "pgrad", "reduce", "finalize",
+                               "adam_u"};
+const char* kStageNames2D[] = {"prep", "assemble", "spd_inverse", "gemm_A", "gemm_A_res",
+                               "gemm_A_fix", "gemm_B", "gemm_B_res", "gemm_B_fix", "gemm_C",
+                               "gemm_D", "gemm_D_res", "gemm_D_fix", "gemm_E", "pgrad", "reduce",
+                               "finalize", "adam_u"};
+constexpr int kMaxStages = 18;
+constexpr int kGemmStages = 11;  // A, A_res, A_fix, B, B_res, B_fix, C, D, D_res, D_fix, E
 
 struct DevSwitch {  // restore the caller's current device on scope exit
   int prev = -1;
@@ -83,7 +89,7 @@ struct gpk_handle {
   int nldet[2] = {0, 0};
   // 2D work
   double *A = nullptr, *Bt = nullptr, *S = nullptr, *R = nullptr, *T1 = nullptr, *T2 = nullptr,
-         *E1 = nullptr, *E2 = nullptr;
+         *X1 = nullptr, *X2 = nullptr, *W1 = nullptr, *W2 = nullptr;  // W: refinement residuals
   double *GK[2] = {}, *GD[2] = {};
   // 1D work
   double *alpha = nullptr, *tvec = nullptr, *beta = nullptr;
@@ -92,7 +98,9 @@ struct gpk_handle {
   double *pgpart = nullptr, *pg = nullptr;
   int bpa = 0;
   GemmDesc* descs = nullptr;
-  Stage st[5];
+  Stage st[kGemmStages];
+  double *Kc[2] = {}, *pst[2] = {};  // kept K (refinement residuals), pivot stats (gate)
+  double* rvec = nullptr;            // 1D refinement residual
   // predict scratch
   GemmDesc* pdescs = nullptr;
 
@@ -146,6 +154,7 @@ static int enqueue_assemble_inverse(gpk_handle* h) {
     aa[a].K = h->K[a];
     aa[a].D = h->D[a];
     aa[a].deriv = deriv;
+    aa[a].Kc = h->Kc[a];
   }
   TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, h->s), "assemble"));
   mark(h, 1);
@@ -158,6 +167,7 @@ static int enqueue_assemble_inverse(gpk_handle* h) {
     sa[a].piv = h->piv[a];
     sa[a].ldet = h->ldet[a];
     sa[a].status = h->status;
+    sa[a].pst = h->pst[a];
   }
   double* fin[2] = {nullptr, nullptr};
   TRY(check_launch(launch_spd_inverse(sa, L.naxes, fin, h->s), "spd_inverse"));
@@ -176,7 +186,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
   int stage = 3;
   const int ac = h->prob.eq == GPK_ALLENCAHN;
   if (L.dim == 2) {
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < kGemmStages; ++k) {
       TRY(check_launch(launch_gemm_batch(h->descs + h->st[k].off, h->st[k].n, h->st[k].maxtiles,
                                          h->sc, h->s, h->st[k].small), "gemm"));
       mark(h, stage++);
@@ -197,24 +207,37 @@ static int enqueue_step(gpk_handle* h, int apply) {
     mark(h, stage++);
   } else {
     const int P = L.p1;
+    // every K^{-1} application gets one step of iterative refinement x += K^{-1}(b - K x),
+    // gated on the pivot spread (gemv skips itself when K is well conditioned)
     GemvDesc g{};
     g.lda = P; g.p = P; g.rows = P; g.alpha = 1.0; g.ac = ac; g.F = h->F; g.U = h->Up;
-    // alpha = K^{-1} u, quad = <u, alpha>          (model_GP_solver_1d.py:92,137)
-    g.A = h->Kinv[0]; g.x = h->Up; g.y = h->alpha; g.epi = EPI_QUAD; g.red = h->red_quad;
-    TRY(check_launch(launch_gemv(g, h->s), "gemv"));
-    mark(h, stage++);
-    // R = D alpha - f (+u(u^2-1)), egap = ||R||^2  (model_GP_solver_1d.py:97,108-116)
-    g.A = h->D[0]; g.x = h->alpha; g.y = h->R; g.epi = EPI_RESID; g.red = h->red_egap;
-    TRY(check_launch(launch_gemv(g, h->s), "gemv"));
-    mark(h, stage++);
+    auto gemv = [&](const double* A, const double* x, double* y, double alpha, const double* C0,
+                    double beta, int epi, double* red, bool gated) -> int {
+      GemvDesc q = g;
+      q.A = A; q.x = x; q.y = y; q.alpha = alpha; q.C0 = C0; q.beta = beta; q.epi = epi; q.red = red;
+      q.gate = gated ? h->pst[0] : nullptr; q.ngate = h->nldet[0];
+      TRY(check_launch(launch_gemv(q, h->s), "gemv"));
+      mark(h, stage++);
+      return GPK_OK;
+    };
+    // alpha = K^{-1} u (refined), quad = <u, alpha>          (model_GP_solver_1d.py:92,137)
+    TRY(gemv(h->Kinv[0], h->Up, h->alpha, 1.0, nullptr, 0.0, EPI_STORE, nullptr, false));
+    TRY(gemv(h->Kc[0], h->alpha, h->rvec, -1.0, h->Up, 1.0, EPI_STORE, nullptr, true));
+    TRY(gemv(h->Kinv[0], h->rvec, h->alpha, 1.0, h->alpha, 1.0, EPI_STORE, nullptr, true));
+    // R = D alpha - f (+u(u^2-1)): egap = ||R||^2 and quad = <u, alpha> in one pass
+    {
+      GemvDesc q = g;
+      q.A = h->D[0]; q.x = h->alpha; q.y = h->R; q.epi = EPI_RESID; q.red = h->red_egap;
+      q.red2 = h->red_quad; q.Q1 = h->Up; q.Q2 = h->alpha;
+      TRY(check_launch(launch_gemv(q, h->s), "gemv"));
+      mark(h, stage++);
+    }
     // t = D^T R (DD_x1 is bitwise symmetric, so D^T = D)
-    g.A = h->D[0]; g.x = h->R; g.y = h->tvec; g.epi = EPI_STORE; g.red = nullptr;
-    TRY(check_launch(launch_gemv(g, h->s), "gemv"));
-    mark(h, stage++);
-    // beta = K^{-1} t
-    g.A = h->Kinv[0]; g.x = h->tvec; g.y = h->beta;
-    TRY(check_launch(launch_gemv(g, h->s), "gemv"));
-    mark(h, stage++);
+    TRY(gemv(h->D[0], h->R, h->tvec, 1.0, nullptr, 0.0, EPI_STORE, nullptr, false));
+    // beta = K^{-1} t (refined)
+    TRY(gemv(h->Kinv[0], h->tvec, h->beta, 1.0, nullptr, 0.0, EPI_STORE, nullptr, false));
+    TRY(gemv(h->Kc[0], h->beta, h->rvec, -1.0, h->tvec, 1.0, EPI_STORE, nullptr, true));
+    TRY(gemv(h->Kinv[0], h->rvec, h->beta, 1.0, h->beta, 1.0, EPI_STORE, nullptr, true));
     PGradArgs pa{};
     pa.x = h->x1; pa.n = L.n1; pa.p = P; pa.kc = h->kc;
     pa.Kinv = h->Kinv[0]; pa.alpha = h->alpha; pa.beta = h->beta; pa.R = h->R;
@@ -239,8 +262,8 @@ static int enqueue_step(gpk_handle* h, int apply) {
   au.L = L; au.hyper = h->hyper; au.llk_weight = h->prob.llk_weight; au.apply = apply; au.ac = ac;
   au.sc = h->sc; au.Up = h->Up; au.bvals = h->bvals; au.bidx = h->bidx; au.nb = h->prob.nb;
   au.params = h->params; au.grad = h->grad; au.m = h->m; au.v = h->v;
-  if (L.dim == 2) { au.E1 = h->E1; au.E2 = h->E2; au.R = h->R; }
-  else { au.E1 = h->alpha; au.E2 = h->beta; au.R = h->R; }
+  if (L.dim == 2) { au.S = h->S; au.X1 = h->X1; au.X2 = h->X2; au.R = h->R; }
+  else { au.S = nullptr; au.X1 = h->alpha; au.X2 = h->beta; au.R = h->R; }
   TRY(check_launch(launch_adam_u(au, h->s), "adam_u"));
   mark(h, stage++);
   h->nstage = stage;
@@ -273,31 +296,75 @@ static int build_descs(gpk_handle* h) {
     h->st[k].small = gemm_use_small(tot16) ? 1 : 0;
     h->st[k].maxtiles = h->st[k].small ? mt16 : mt32;
   };
-  // Stage A: A = K1^{-1} U, Bt = U K2^{-1}        (model_GP_solver_2d.py:104-105)
+  // Every solve against K (JAX: LU solves, model_GP_solver_2d.py:104-105 and the reverse
+  // pass) is X = K^{-1} B (MFMA) plus one refinement X += K^{-1}(B - K X), whose two GEMMs are
+  // gated on the factor's pivot spread (skipped when K is well conditioned, e.g. 256^2).
+  const int n1 = L.n1, n2 = L.n2;
+  auto gate = [&](GemmDesc g, int axis) {
+    g.gate = h->pst[axis];
+    g.ngate = h->nldet[axis];
+    return g;
+  };
+  // Stage A: A = K1^{-1} U, Bt = U K2^{-1}                       (2d.py:104-105)
   begin(0);
   d.push_back(mk(h->Kinv[0], P1, 0, h->Up, P2, 0, h->A, P2, P1, P2, P1));
   d.push_back(mk(h->Up, P2, 0, h->Kinv[1], P2, 0, h->Bt, P2, P1, P2, P2));
   end(0);
-  // Stage B: S = A K2^{-1} (+<U,S>);  R = beta D1 A + Bt D2^T - F (+AC) (+||R||^2)  (:112-143)
-  begin(1);
+  begin(1);  // residuals W1 = U - K1 A, W2 = U - Bt K2
   {
-    GemmDesc g = mk(h->A, P2, 0, h->Kinv[1], P2, 0, h->S, P2, P1, P2, P2);
-    g.epi = EPI_QUAD; g.U = h->Up; g.ldf = P2; g.red = h->red_quad;
-    d.push_back(g);
+    GemmDesc g = mk(h->Kc[0], P1, 0, h->A, P2, 0, h->W1, P2, P1, P2, P1);
+    g.alpha = -1.0; g.beta = 1.0; g.C0 = h->Up; g.ldc0 = P2;
+    d.push_back(gate(g, 0));
+    GemmDesc g2 = mk(h->Bt, P2, 0, h->Kc[1], P2, 0, h->W2, P2, P1, P2, P2);
+    g2.alpha = -1.0; g2.beta = 1.0; g2.C0 = h->Up; g2.ldc0 = P2;
+    d.push_back(gate(g2, 1));
+  }
+  end(1);
+  begin(2);  // A += K1^{-1} W1, Bt += W2 K2^{-1}  (in place)
+  {
+    GemmDesc g = mk(h->Kinv[0], P1, 0, h->W1, P2, 0, h->A, P2, P1, P2, P1);
+    g.beta = 1.0; g.C0 = h->A; g.ldc0 = P2;
+    d.push_back(gate(g, 0));
+    GemmDesc g2 = mk(h->W2, P2, 0, h->Kinv[1], P2, 0, h->Bt, P2, P1, P2, P2);
+    g2.beta = 1.0; g2.C0 = h->Bt; g2.ldc0 = P2;
+    d.push_back(gate(g2, 1));
+  }
+  end(2);
+  // Stage B: S = A K2^{-1};  R = beta D1 A + Bt D2^T - F (+AC), ||R||^2 and the prior's
+  // quadratic term sum(A * Bt) (2d.py:112-143, :161) from the same tile loop
+  begin(3);
+  {
+    d.push_back(mk(h->A, P2, 0, h->Kinv[1], P2, 0, h->S, P2, P1, P2, P2));
     GemmDesc r = mk(h->D[0], P1, 0, h->A, P2, 0, h->R, P2, P1, P2, P1);
     r.alpha = beta;
     r.A2 = h->Bt; r.lda2 = P2; r.ta2 = 0; r.B2 = h->D[1]; r.ldb2 = P2; r.tb2 = 1; r.K2 = P2;
     r.alpha2 = 1.0;
     r.epi = EPI_RESID; r.F = h->F; r.U = h->Up; r.ldf = P2; r.ac = ac; r.red = h->red_egap;
+    r.red2 = h->red_quad; r.Q1 = h->A; r.Q2 = h->Bt;
     d.push_back(r);
   }
-  end(1);
-  h->nquad = h->negap = h->st[1].small ? (P1 / 16) * (P2 / 16) : (P1 / 32) * (P2 / 32);
-  // Stage C: T1 = D1^T R, T2 = R D2, G_D1 = v beta R A^T, G_D2 = v R^T Bt   (Appendix A)
-  begin(2);
-  d.push_back(mk(h->D[0], P1, 1, h->R, P2, 0, h->T1, P2, P1, P2, P1));
-  d.push_back(mk(h->R, P2, 0, h->D[1], P2, 0, h->T2, P2, P1, P2, P2));
+  end(3);
+  begin(4);  // W1 = A - S K2
   {
+    GemmDesc g = mk(h->S, P2, 0, h->Kc[1], P2, 0, h->W1, P2, P1, P2, P2);
+    g.alpha = -1.0; g.beta = 1.0; g.C0 = h->A; g.ldc0 = P2;
+    d.push_back(gate(g, 1));
+  }
+  end(4);
+  begin(5);  // S += W1 K2^{-1}
+  {
+    GemmDesc g = mk(h->W1, P2, 0, h->Kinv[1], P2, 0, h->S, P2, P1, P2, P2);
+    g.beta = 1.0; g.C0 = h->S; g.ldc0 = P2;
+    d.push_back(gate(g, 1));
+  }
+  end(5);
+  // Stage C: T1 = beta D1^T R, T2 = R D2, G_D1 = v beta R A^T, G_D2 = v R^T Bt  (Appendix A)
+  begin(6);
+  {
+    GemmDesc t1 = mk(h->D[0], P1, 1, h->R, P2, 0, h->T1, P2, P1, P2, P1);
+    t1.alpha = beta;
+    d.push_back(t1);
+    d.push_back(mk(h->R, P2, 0, h->D[1], P2, 0, h->T2, P2, P1, P2, P2));
     GemmDesc g = mk(h->R, P2, 0, h->A, P2, 1, h->GD[0], P1, P1, P1, P2);
     g.alpha = beta; g.vscale = 1;
     d.push_back(g);
@@ -305,29 +372,50 @@ static int build_descs(gpk_handle* h) {
     g2.vscale = 1;
     d.push_back(g2);
   }
-  end(2);
-  // Stage D: E1 = S/2 + v beta K1^{-1} T1;  E2 = S/2 + v T2 K2^{-1}
-  begin(3);
+  end(6);
+  // Stage D: X1 = K1^{-1} T1, X2 = T2 K2^{-1} (refined)
+  begin(7);
+  d.push_back(mk(h->Kinv[0], P1, 0, h->T1, P2, 0, h->X1, P2, P1, P2, P1));
+  d.push_back(mk(h->T2, P2, 0, h->Kinv[1], P2, 0, h->X2, P2, P1, P2, P2));
+  end(7);
+  begin(8);
   {
-    GemmDesc g = mk(h->Kinv[0], P1, 0, h->T1, P2, 0, h->E1, P2, P1, P2, P1);
-    g.alpha = beta; g.vscale = 1; g.epi = EPI_HALFS; g.C0 = h->S; g.ldc0 = P2;
+    GemmDesc g = mk(h->Kc[0], P1, 0, h->X1, P2, 0, h->W1, P2, P1, P2, P1);
+    g.alpha = -1.0; g.beta = 1.0; g.C0 = h->T1; g.ldc0 = P2;
+    d.push_back(gate(g, 0));
+    GemmDesc g2 = mk(h->X2, P2, 0, h->Kc[1], P2, 0, h->W2, P2, P1, P2, P2);
+    g2.alpha = -1.0; g2.beta = 1.0; g2.C0 = h->T2; g2.ldc0 = P2;
+    d.push_back(gate(g2, 1));
+  }
+  end(8);
+  begin(9);
+  {
+    GemmDesc g = mk(h->Kinv[0], P1, 0, h->W1, P2, 0, h->X1, P2, P1, P2, P1);
+    g.beta = 1.0; g.C0 = h->X1; g.ldc0 = P2;
+    d.push_back(gate(g, 0));
+    GemmDesc g2 = mk(h->W2, P2, 0, h->Kinv[1], P2, 0, h->X2, P2, P1, P2, P2);
+    g2.beta = 1.0; g2.C0 = h->X2; g2.ldc0 = P2;
+    d.push_back(gate(g2, 1));
+  }
+  end(9);
+  // Stage E: G_K1 = c N2/2 K1^{-1} - (S/2 + v X1) A^T;  G_K2 = c N1/2 K2^{-1} - (S/2 + v X2)^T Bt
+  begin(10);
+  {
+    GemmDesc g = mk(h->S, P2, 0, h->A, P2, 1, h->GK[0], P1, P1, P1, P2);
+    g.alpha = -0.5;
+    g.A2 = h->X1; g.lda2 = P2; g.B2 = h->A; g.ldb2 = P2; g.tb2 = 1; g.K2 = P2;
+    g.alpha2 = -1.0; g.vscale2 = 1;
+    g.beta = 0.5 * h->prob.logdet * n2; g.C0 = h->Kinv[0]; g.ldc0 = P1;
     d.push_back(g);
-    GemmDesc g2 = mk(h->T2, P2, 0, h->Kinv[1], P2, 0, h->E2, P2, P1, P2, P2);
-    g2.vscale = 1; g2.epi = EPI_HALFS; g2.C0 = h->S; g2.ldc0 = P2;
+    GemmDesc g2 = mk(h->S, P2, 1, h->Bt, P2, 0, h->GK[1], P2, P2, P2, P1);
+    g2.alpha = -0.5;
+    g2.A2 = h->X2; g2.lda2 = P2; g2.ta2 = 1; g2.B2 = h->Bt; g2.ldb2 = P2; g2.K2 = P1;
+    g2.alpha2 = -1.0; g2.vscale2 = 1;
+    g2.beta = 0.5 * h->prob.logdet * n1; g2.C0 = h->Kinv[1]; g2.ldc0 = P2;
     d.push_back(g2);
   }
-  end(3);
-  // Stage E: G_K1 = c N2/2 K1^{-1} - E1 A^T;  G_K2 = c N1/2 K2^{-1} - E2^T Bt
-  begin(4);
-  {
-    GemmDesc g = mk(h->E1, P2, 0, h->A, P2, 1, h->GK[0], P1, P1, P1, P2);
-    g.alpha = -1.0; g.beta = 0.5 * h->prob.logdet * L.n2; g.C0 = h->Kinv[0]; g.ldc0 = P1;
-    d.push_back(g);
-    GemmDesc g2 = mk(h->E2, P2, 1, h->Bt, P2, 0, h->GK[1], P2, P2, P2, P1);
-    g2.alpha = -1.0; g2.beta = 0.5 * h->prob.logdet * L.n1; g2.C0 = h->Kinv[1]; g2.ldc0 = P2;
-    d.push_back(g2);
-  }
-  end(4);
+  end(10);
+  h->nquad = h->negap = h->st[3].small ? (P1 / 16) * (P2 / 16) : (P1 / 32) * (P2 / 32);
   TRY(h->alloc(&h->descs, d.size()));
   HIPCHK(hipMemcpyAsync(h->descs, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice, h->s));
   HIPCHK(hipStreamSynchronize(h->s));
@@ -546,11 +634,14 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
     A_(h->D[a], (size_t)P * P);
     A_(h->piv[a], (size_t)P * 32);
     A_(h->ldet[a], P / 32);
+    A_(h->Kc[a], (size_t)P * P);
+    A_(h->pst[a], 2 * (P / 32));
     h->nldet[a] = P / 32;
   }
   if (L.dim == 2) {
     A_(h->A, nup); A_(h->Bt, nup); A_(h->S, nup); A_(h->R, nup);
-    A_(h->T1, nup); A_(h->T2, nup); A_(h->E1, nup); A_(h->E2, nup);
+    A_(h->T1, nup); A_(h->T2, nup); A_(h->X1, nup); A_(h->X2, nup);
+    A_(h->W1, nup); A_(h->W2, nup);
     for (int a = 0; a < 2; ++a) {
       const int P = a == 0 ? P1 : P2;
       A_(h->GK[a], (size_t)P * P);
@@ -558,7 +649,7 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
     }
     h->nquad = h->negap = (P1 / 16) * (P2 / 16);  // upper bound (16x16 tiles); set in build_descs
   } else {
-    A_(h->alpha, P1); A_(h->R, P1); A_(h->tvec, P1); A_(h->beta, P1);
+    A_(h->alpha, P1); A_(h->R, P1); A_(h->tvec, P1); A_(h->beta, P1); A_(h->rvec, P1);
     h->nquad = h->negap = gemv_blocks(P1);
   }
   A_(h->red_quad, h->nquad);
@@ -739,37 +830,54 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
   if (L.dim == 1) {
     double* alpha;
     if ((r = dalloc(&alpha, P1)) || (r = dalloc(&res, M1p))) { cleanup(); return r; }
-    GemvDesc g{};
-    g.A = h->Kinv[0]; g.lda = P1; g.x = h->Up; g.y = alpha; g.p = P1; g.rows = P1; g.alpha = 1.0;
-    g.epi = EPI_STORE;
-    (void)launch_gemv(g, h->s);
-    g.A = Kmn1; g.x = alpha; g.y = res; g.rows = m1;  // preds = Kmn K^{-1} u  (1d.py:176-179)
-    (void)launch_gemv(g, h->s);
+    double* rv;
+    if ((r = dalloc(&rv, P1))) { cleanup(); return r; }
+    auto gv = [&](const double* A, const double* x, double* y, int rows, double al, const double* C0,
+                  double be) {
+      GemvDesc g{};
+      g.A = A; g.lda = P1; g.x = x; g.y = y; g.p = P1; g.rows = rows; g.alpha = al;
+      g.C0 = C0; g.beta = be; g.epi = EPI_STORE;
+      (void)launch_gemv(g, h->s);
+    };
+    // alpha = K^{-1} u with one refinement step (matches solve() accuracy; 1d.py:176-179)
+    gv(h->Kinv[0], h->Up, alpha, P1, 1.0, nullptr, 0.0);
+    gv(h->Kc[0], alpha, rv, P1, -1.0, h->Up, 1.0);
+    gv(h->Kinv[0], rv, alpha, P1, 1.0, alpha, 1.0);
+    gv(Kmn1, alpha, res, m1, 1.0, nullptr, 0.0);  // preds = Kmn K^{-1} u
     (void)hipMemcpyAsync(out, res, m1 * sizeof(double), hipMemcpyDeviceToHost, h->s);
   } else {
     // U_pred = Kmn1 (K1^{-1} U K2^{-1}) Kmn2^T   (model_GP_solver_2d.py:185-220)
     const int M2p = pad_up(m2), P2 = L.p2;
-    double *dx2, *Kmn2, *Aw, *Sw, *Mw;
+    double *dx2, *Kmn2, *Aw, *Sw, *Mw, *Rw;
     if ((r = dalloc(&dx2, m2)) || (r = dalloc(&Kmn2, (size_t)M2p * P2)) || (r = dalloc(&Aw, (size_t)P1 * P2)) ||
         (r = dalloc(&Sw, (size_t)P1 * P2)) || (r = dalloc(&Mw, (size_t)M1p * P2)) ||
-        (r = dalloc(&res, (size_t)M1p * M2p))) { cleanup(); return r; }
+        (r = dalloc(&Rw, (size_t)P1 * P2)) || (r = dalloc(&res, (size_t)M1p * M2p))) { cleanup(); return r; }
     (void)hipMemcpyAsync(dx2, xte2, m2 * sizeof(double), hipMemcpyHostToDevice, h->s);
     (void)launch_cross(h->prob.kind, L.q, dx2, m2, h->x2, L.n2, P2, h->kc + 1, 0.0, 0, Kmn2, nullptr, h->s);
-    GemmDesc d[4] = {};
+    GemmDesc d[8] = {};
     auto mk = [](GemmDesc& g, const double* A, int lda, int ta, const double* B, int ldb, int tb,
                  double* C, int ldc, int M, int N, int K) {
       g.A = A; g.lda = lda; g.ta = ta; g.B = B; g.ldb = ldb; g.tb = tb; g.C = C; g.ldc = ldc;
       g.M = M; g.N = N; g.K = K; g.alpha = 1.0; g.epi = EPI_STORE;
     };
+    // A = K1^{-1} U and S = A K2^{-1}, each with one refinement step (solve() accuracy)
     mk(d[0], h->Kinv[0], P1, 0, h->Up, P2, 0, Aw, P2, P1, P2, P1);
-    mk(d[1], Aw, P2, 0, h->Kinv[1], P2, 0, Sw, P2, P1, P2, P2);
-    mk(d[2], Kmn1, P1, 0, Sw, P2, 0, Mw, P2, M1p, P2, P1);
-    mk(d[3], Mw, P2, 0, Kmn2, P2, 1, res, M2p, M1p, M2p, P2);
+    mk(d[1], h->Kc[0], P1, 0, Aw, P2, 0, Rw, P2, P1, P2, P1);          // Rw = U - K1 A
+    d[1].alpha = -1.0; d[1].beta = 1.0; d[1].C0 = h->Up; d[1].ldc0 = P2;
+    mk(d[2], h->Kinv[0], P1, 0, Rw, P2, 0, Aw, P2, P1, P2, P1);        // A += K1^{-1} Rw
+    d[2].beta = 1.0; d[2].C0 = Aw; d[2].ldc0 = P2;
+    mk(d[3], Aw, P2, 0, h->Kinv[1], P2, 0, Sw, P2, P1, P2, P2);
+    mk(d[4], Sw, P2, 0, h->Kc[1], P2, 0, Rw, P2, P1, P2, P2);          // Rw = A - S K2
+    d[4].alpha = -1.0; d[4].beta = 1.0; d[4].C0 = Aw; d[4].ldc0 = P2;
+    mk(d[5], Rw, P2, 0, h->Kinv[1], P2, 0, Sw, P2, P1, P2, P2);        // S += Rw K2^{-1}
+    d[5].beta = 1.0; d[5].C0 = Sw; d[5].ldc0 = P2;
+    mk(d[6], Kmn1, P1, 0, Sw, P2, 0, Mw, P2, M1p, P2, P1);
+    mk(d[7], Mw, P2, 0, Kmn2, P2, 1, res, M2p, M1p, M2p, P2);
     GemmDesc* dd;
     if (hipMalloc(&dd, sizeof(d)) != hipSuccess) { cleanup(); return fail(GPK_ENOMEM, "hipMalloc"); }
     tmp.push_back(dd);
     (void)hipMemcpyAsync(dd, d, sizeof(d), hipMemcpyHostToDevice, h->s);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 8; ++k) {
       const long t16 = (long)(d[k].M / 16) * (d[k].N / 16);
       const int small = gemm_use_small(t16) ? 1 : 0;
       (void)launch_gemm_batch(dd + k, 1, small ? (int)t16 : (d[k].M / 32) * (d[k].N / 32), h->sc, h->s, small);
@@ -817,8 +925,8 @@ int gpk_profile_stages(gpk_handle* h, int32_t iters, double* out_us, int32_t cap
 
 const char* gpk_stage_name(const gpk_handle* h, int32_t stage) {
   if (!h || stage < 0) return "?";
-  if (h->L.dim == 2) return stage < 12 ? kStageNames2D[stage] : "?";
-  return stage < 11 ? kStageNames1D[stage] : "?";
+  if (h->L.dim == 2) return stage < 18 ? kStageNames2D[stage] : "?";
+  return stage < 15 ? kStageNames1D[stage] : "?";
 }
 
 int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us) {
@@ -837,13 +945,14 @@ int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us) {
     for (int a = 0; a < L.naxes; ++a) {
       aa[a].x = a == 0 ? h->x1 : h->x2; aa[a].n = a == 0 ? L.n1 : L.n2; aa[a].p = a == 0 ? L.p1 : L.p2;
       aa[a].kc = h->kc + a; aa[a].jitter = h->prob.jitter; aa[a].K = h->K[a]; aa[a].D = h->D[a];
-      aa[a].deriv = deriv;
+      aa[a].deriv = deriv; aa[a].Kc = nullptr;
     }
     TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, h->s), "assemble"));
     SpdArgs sa[2];
     for (int a = 0; a < L.naxes; ++a) {
       sa[a].X = h->K[a]; sa[a].Y = h->Kb[a]; sa[a].p = a == 0 ? L.p1 : L.p2; sa[a].n = a == 0 ? L.n1 : L.n2;
       sa[a].piv = h->piv[a]; sa[a].ldet = h->ldet[a]; sa[a].status = h->status;
+      sa[a].pst = h->pst[a];
     }
     double* fin[2];
     HIPCHK(hipEventRecord(e0, h->s));
@@ -857,6 +966,212 @@ int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us) {
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   *avg_us = total / iters;
+  return read_status(h);
+}
+
+int gpk_kernel_pairs(int32_t kind, int32_t deriv, const double* x1, const double* x2, int64_t n,
+                     const double* logw, const double* logls, const double* freq, int32_t q,
+                     double* out) {
+  if (kind < 0 || kind > 3) return fail(GPK_EINVAL, "Invalid Kernel");
+  if (deriv < 0 || deriv > 2) return fail(GPK_EINVAL, "deriv must be 0, 1 or 2");
+  if (n <= 0 || q <= 0 || q > QMAX) return fail(GPK_EINVAL, "bad sizes (0 < q <= 64)");
+  if (!x1 || !x2 || !logw || !logls || !freq || !out) return fail(GPK_EINVAL, "NULL pointer argument");
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  TRY(check_device(dev));
+  AxisConst hk;
+  host_axis_const(logw, logls, freq, q, &hk);
+  double *d1 = nullptr, *d2 = nullptr, *dout = nullptr;
+  AxisConst* dkc = nullptr;
+  auto cleanup = [&]() {
+    if (d1) (void)hipFree(d1);
+    if (d2) (void)hipFree(d2);
+    if (dout) (void)hipFree(dout);
+    if (dkc) (void)hipFree(dkc);
+  };
+  const size_t bytes = (size_t)n * sizeof(double);
+  if (hipMalloc(&d1, bytes) != hipSuccess || hipMalloc(&d2, bytes) != hipSuccess ||
+      hipMalloc(&dout, bytes) != hipSuccess || hipMalloc(&dkc, sizeof(AxisConst)) != hipSuccess) {
+    cleanup();
+    return fail(GPK_ENOMEM, "hipMalloc failed");
+  }
+  hipError_t e = hipMemcpy(d1, x1, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d2, x2, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dkc, &hk, sizeof(AxisConst), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_pairs(kind, q, d1, d2, n, dkc, deriv, dout, 0);
+  if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+  cleanup();
+  if (e != hipSuccess) return fail(GPK_EHIP, std::string("kernel_pairs: ") + hipGetErrorString(e));
+  return GPK_OK;
+}
+
+int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
+  if (!h || !out) return fail(GPK_EINVAL, "NULL argument");
+  const Layout& L = h->L;
+  const int64_t n1 = L.n1, n2 = L.n2;
+  int64_t want;
+  if (L.dim == 2) {
+    const int64_t sizes[6] = {n1 * n1, n2 * n2, n1 * n2, n2 * n1, n1 * n2, n1 * n2};
+    if (what < 0 || what > 5) return fail(GPK_EINVAL, "what must be 0..5 (2D)");
+    want = sizes[what];
+  } else {
+    if (what != 0 && what != 2 && what != 4) return fail(GPK_EINVAL, "what must be 0, 2 or 4 (1D)");
+    want = what == 0 ? n1 * n1 : n1;
+  }
+  if (n != want) return fail(GPK_EINVAL, "output size mismatch");
+  DevSwitch ds(h->dev);
+  std::vector<double> host;
+  double* tmp = nullptr;
+  auto cleanup = [&]() {
+    if (tmp) (void)hipFree(tmp);
+  };
+  if (what <= 1) {  // K factor: assemble at the current params (kappa + jitter I)
+    const int a = what;
+    const int na = a == 0 ? L.n1 : L.n2;
+    TRY(check_launch(launch_prep2(h->params, L, h->kc, h->sc, h->count, 0, h->hyper.b1, h->hyper.b2, h->s), "prep"));
+    HIPCHK(hipMalloc(&tmp, (size_t)na * na * sizeof(double)));
+    const double* xa = a == 0 ? h->x1 : h->x2;
+    int rc = check_launch(launch_cross(h->prob.kind, L.q, xa, na, xa, na, na, h->kc + a, h->prob.jitter,
+                                       0, tmp, nullptr, h->s), "cross");
+    if (rc == GPK_OK && hipMemcpyAsync(out, tmp, n * sizeof(double), hipMemcpyDeviceToHost, h->s) != hipSuccess)
+      rc = fail(GPK_EHIP, "copy");
+    if (rc == GPK_OK && hipStreamSynchronize(h->s) != hipSuccess) rc = fail(GPK_EHIP, "sync");
+    cleanup();
+    return rc;
+  }
+  double loss = 0.0;
+  TRY(gpk_loss_grad(h, &loss, nullptr));  // device buffers now hold the forward quantities
+  if (L.dim == 1) {
+    const int P = L.p1;
+    const double* src = h->alpha;
+    if (what == 4) {  // u_xx = D alpha
+      HIPCHK(hipMalloc(&tmp, P * sizeof(double)));
+      GemvDesc g{};
+      g.A = h->D[0]; g.lda = P; g.x = h->alpha; g.y = tmp; g.p = P; g.rows = P; g.alpha = 1.0;
+      g.epi = EPI_STORE;
+      int rc = check_launch(launch_gemv(g, h->s), "gemv");
+      if (rc) { cleanup(); return rc; }
+      src = tmp;
+    }
+    hipError_t e = hipMemcpyAsync(out, src, n * sizeof(double), hipMemcpyDeviceToHost, h->s);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->s);
+    cleanup();
+    if (e != hipSuccess) return fail(GPK_EHIP, hipGetErrorString(e));
+    return GPK_OK;
+  }
+  const int P1 = L.p1, P2 = L.p2;
+  const double* src = (what == 3) ? h->Bt : h->A;
+  if (what >= 4) {  // U_xx = D1 A  /  U_yy = Bt D2^T
+    HIPCHK(hipMalloc(&tmp, (size_t)P1 * P2 * sizeof(double) + sizeof(GemmDesc)));
+    GemmDesc g{};
+    if (what == 4) {
+      g.A = h->D[0]; g.lda = P1; g.B = h->A; g.ldb = P2; g.K = P1;
+    } else {
+      g.A = h->Bt; g.lda = P2; g.B = h->D[1]; g.ldb = P2; g.tb = 1; g.K = P2;
+    }
+    g.C = tmp; g.ldc = P2; g.M = P1; g.N = P2; g.alpha = 1.0; g.epi = EPI_STORE;
+    GemmDesc* dd = reinterpret_cast<GemmDesc*>(tmp + (size_t)P1 * P2);
+    hipError_t e = hipMemcpyAsync(dd, &g, sizeof(g), hipMemcpyHostToDevice, h->s);
+    const long t16 = (long)(P1 / 16) * (P2 / 16);
+    const int small = gemm_use_small(t16) ? 1 : 0;
+    if (e == hipSuccess)
+      e = launch_gemm_batch(dd, 1, small ? (int)t16 : (P1 / 32) * (P2 / 32), h->sc, h->s, small);
+    if (e != hipSuccess) { cleanup(); return fail(GPK_EHIP, hipGetErrorString(e)); }
+    src = tmp;
+  }
+  host.resize((size_t)P1 * P2);
+  hipError_t e = hipMemcpyAsync(host.data(), src, host.size() * sizeof(double), hipMemcpyDeviceToHost, h->s);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->s);
+  cleanup();
+  if (e != hipSuccess) return fail(GPK_EHIP, hipGetErrorString(e));
+  for (int64_t i = 0; i < n1; ++i)
+    for (int64_t j = 0; j < n2; ++j) {
+      const double v = host[(size_t)i * P2 + j];
+      if (what == 3)
+        out[j * n1 + i] = v;  // K2inv_Ut = (U K2^{-1})^T
+      else
+        out[i * n2 + j] = v;
+    }
+  return GPK_OK;
+}
+
+int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg_us,
+                     double* alg_flops, double* alg_bytes) {
+  if (!h || !name || !avg_us || !alg_flops || !alg_bytes || iters <= 0)
+    return fail(GPK_EINVAL, "bad argument");
+  const std::string nm(name);
+  const Layout& L = h->L;
+  // one full step (no update) so every kernel's inputs are valid
+  double loss = 0.0;
+  TRY(gpk_loss_grad(h, &loss, nullptr));
+  DevSwitch ds(h->dev);
+  const int deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
+  AssembleArgs aa[2];
+  SpdArgs sa[2];
+  for (int a = 0; a < L.naxes; ++a) {
+    aa[a].x = a == 0 ? h->x1 : h->x2; aa[a].n = a == 0 ? L.n1 : L.n2; aa[a].p = a == 0 ? L.p1 : L.p2;
+    aa[a].kc = h->kc + a; aa[a].jitter = h->prob.jitter; aa[a].K = h->K[a]; aa[a].D = h->D[a];
+    aa[a].deriv = deriv; aa[a].Kc = nullptr;
+    sa[a].X = h->K[a]; sa[a].Y = h->Kb[a]; sa[a].p = aa[a].p; sa[a].n = aa[a].n;
+    sa[a].piv = h->piv[a]; sa[a].ldet = h->ldet[a]; sa[a].status = h->status;
+      sa[a].pst = h->pst[a];
+  }
+  std::function<hipError_t()> launch;
+  double flops = 0.0, bytes = 0.0;
+  const double n1 = L.n1, n2 = L.dim == 2 ? L.n2 : 0.0;
+  if (nm == "sweep") {
+    // re-assemble K and factor pivot 0, then time sweep 0 (idempotent: X -> Y, piv[1]).
+    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, h->s), "assemble"));
+    TRY(check_launch(launch_spd_stage(sa, L.naxes, -1, h->s), "pivot_init"));
+    launch = [&]() { return launch_spd_stage(sa, L.naxes, 0, h->s); };
+    // potrf+potri-equivalent flops (n^3 per factor) spread over the T = p/32 sweeps;
+    // HBM bytes: read X + write Y per factor
+    for (int a = 0; a < L.naxes; ++a) {
+      const double n = a == 0 ? n1 : n2;
+      flops += n * n * n / ((a == 0 ? L.p1 : L.p2) / 32);
+      bytes += 16.0 * n * n;
+    }
+  } else if (nm == "assemble") {
+    launch = [&]() { return launch_assemble(h->prob.kind, L.q, aa, L.naxes, h->s); };
+    // K and D written (8 B each per element); flops not counted (transcendental-bound)
+    for (int a = 0; a < L.naxes; ++a) { const double n = a == 0 ? n1 : n2; bytes += 16.0 * n * n; }
+  } else if (nm == "gemm_B" && L.dim == 2) {
+    launch = [&]() {
+      return launch_gemm_batch(h->descs + h->st[3].off, h->st[3].n, h->st[3].maxtiles, h->sc, h->s,
+                               h->st[3].small);
+    };
+    // S = A K2^{-1} (2 n1 n2^2); R = D1 A + Bt D2^T (2 n1^2 n2 + 2 n1 n2^2)
+    flops = 2 * n1 * n2 * n2 + 2 * n1 * n1 * n2 + 2 * n1 * n2 * n2;
+    // reads A, K2^{-1}, D1, Bt, D2, F, U; writes S, R
+    bytes = 8.0 * (n1 * n2 + n2 * n2 + n1 * n1 + n1 * n2 + n2 * n2 + 2 * n1 * n2 + 2 * n1 * n2);
+  } else if (nm == "pgrad" && L.dim == 2) {
+    PGradArgs pa[2];
+    for (int a = 0; a < 2; ++a) {
+      pa[a] = PGradArgs{};
+      pa[a].x = a == 0 ? h->x1 : h->x2; pa[a].n = a == 0 ? L.n1 : L.n2; pa[a].p = a == 0 ? L.p1 : L.p2;
+      pa[a].kc = h->kc + a; pa[a].GK = h->GK[a]; pa[a].GD = h->GD[a]; pa[a].deriv = deriv;
+      pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
+    }
+    launch = [&, pa]() mutable { return launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s); };
+    bytes = 16.0 * (n1 * n1 + n2 * n2);  // G_K, G_D read
+  } else {
+    return fail(GPK_EINVAL, "unknown kernel name (sweep | assemble | gemm_B | pgrad[2D])");
+  }
+  HIPCHK(launch());  // warm
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, h->s));
+  for (int it = 0; it < iters; ++it) HIPCHK(launch());
+  HIPCHK(hipEventRecord(e1, h->s));
+  HIPCHK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *avg_us = ms * 1000.0 / iters;
+  *alg_flops = flops;
+  *alg_bytes = bytes;
   return read_status(h);
 }
 

@@ -87,16 +87,19 @@ struct AssembleArgs {
   int p;                 // padded size (leading dimension)
   const AxisConst* kc;   // device
   double jitter;
-  double* K;             // [p*p]
+  double* K;             // [p*p]  (consumed in place by the SPD inverse)
+  double* Kc;            // [p*p]  kept copy of K for iterative refinement (nullable)
   double* D;             // [p*p]
   int deriv;             // 1 or 2 (0: K only)
 };
 hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, hipStream_t s);
+hipError_t launch_pairs(int kind, int q, const double* x1, const double* x2, long n,
+                        const AxisConst* kc, int deriv, double* out, hipStream_t s);
 hipError_t launch_cross(int kind, int q, const double* xr, int nr, const double* xc, int nc,
                         int ld, const AxisConst* kc, double jitter, int deriv, double* K,
                         double* D, hipStream_t s);
 
-// SPD inverse by blocked Gauss-Jordan sweeps (pivot blocks factored in LDS).
+// SPD inverse by blocked Cholesky-Gauss-Jordan sweeps (pivot blocks factored in LDS).
 struct SpdArgs {
   double* X;       // [p*p] input (assembled K), ping
   double* Y;       // [p*p] pong
@@ -104,17 +107,23 @@ struct SpdArgs {
   int n;           // true dim (pads are identity)
   double* piv;     // [(p/NB) * NB*NB] pivot-block inverse scratch
   double* ldet;    // [p/NB] logdet contribution of each pivot block
+  double* pst;     // [p/NB][2] min / max Cholesky pivot (L_ii^2) of each block
   int* status;     // nonzero => not positive definite
 };
 // Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.
 hipError_t launch_spd_inverse(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
+hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
+
+// Iterative-refinement gate: a refinement GEMM/GEMV runs only when the factor's Cholesky
+// pivot spread max(L_ii^2)/min(L_ii^2) (a lower bound on cond(K)) exceeds this.
+constexpr double REFINE_PIVOT_RATIO = 100.0;
 
 // Batched fp64 MFMA GEMM with fused epilogues.
 enum Epi {
   EPI_STORE = 0,   // C = alpha*P1 + alpha2*P2 + beta*C0
   EPI_RESID = 1,   // C = alpha*P1 + alpha2*P2 - F (+ U(U^2-1) if ac) ; red += sum C^2
-  EPI_QUAD = 2,    // C = alpha*P1 ; red += sum C*U
-  EPI_HALFS = 3,   // C = alpha*v*P1 + 0.5*S     (v from StepScalars)
+                   //     (+ red2 += sum Q1*Q2 when red2 != NULL)
+  EPI_QUAD = 2,    // C = alpha*P1 + beta*C0 ; red += sum C*U
 };
 struct GemmDesc {
   const double* A; const double* B; int lda, ldb, ta, tb;
@@ -126,8 +135,10 @@ struct GemmDesc {
   int epi;
   int ac;                   // EPI_RESID: Allen-Cahn term
   const double* F; const double* U; int ldf; // epilogue operands
-  int vscale;               // multiply alpha by v (StepScalars) when 1
+  int vscale, vscale2;      // multiply alpha / alpha2 by v (StepScalars) when 1
   double* red;              // per-tile partial sums, [tiles] (nullable)
+  double* red2; const double* Q1; const double* Q2;  // EPI_RESID: sum Q1*Q2 (quad term)
+  const double* gate; int ngate;  // pivot stats [ngate][2]; skip unless spread > ratio
 };
 // small = 1: 16x16-tile latency kernel (max_tiles counts 16x16 tiles); 0: 32x32 LDS-tiled
 hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles,
@@ -135,14 +146,27 @@ hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles
 // heuristic: use the 16x16 latency kernel while the whole stage has few enough tiles
 inline bool gemm_use_small(long tiles16_total) { return tiles16_total <= 16384; }
 
-// GEMV y = alpha * A x (A padded p x p, op N), optional epilogues like GEMM
+__device__ __forceinline__ bool refine_gate_open(const double* gate, int ngate) {
+  if (!gate) return true;
+  double mn = gate[0], mx = gate[1];
+  for (int k = 1; k < ngate; ++k) {
+    mn = fmin(mn, gate[2 * k]);
+    mx = fmax(mx, gate[2 * k + 1]);
+  }
+  return mx > REFINE_PIVOT_RATIO * mn;
+}
+
+// GEMV y = alpha * A x + beta * C0 (A padded, op N), optional epilogues like GEMM
 struct GemvDesc {
   const double* A; int lda; const double* x; double* y; int p; int rows;
   double alpha;
+  const double* C0; double beta;
   int epi;           // EPI_STORE / EPI_RESID / EPI_QUAD
   int ac;
   const double* F; const double* U;
   double* red;       // per-block partials
+  double* red2; const double* Q1; const double* Q2;  // per-block partials of sum Q1*Q2
+  const double* gate; int ngate;
 };
 hipError_t launch_gemv(const GemvDesc& d, hipStream_t s);
 int gemv_blocks(int rows);

@@ -106,8 +106,23 @@ struct SpdBatch {
   int T[2];       // p / 32
   double* piv[2]; // [T][32*32] L^{-1} of each pivot block
   double* ldet[2];
+  double* pst[2];  // [T][2] min / max pivot of each block (refinement gate)
+  int n[2];        // true size: pivots of padded rows (exactly 1) are left out of pst
   int* status[2];
 };
+
+// thread 0: min / max of the real (unpadded) pivots of block k
+__device__ __forceinline__ void write_pivot_stats(const double* pv, int k, int n, double* pst) {
+  double mn = 1.0e300, mx = 0.0;
+  for (int j = 0; j < 32; ++j) {
+    if (k * 32 + j >= n) break;
+    mn = fmin(mn, pv[j]);
+    mx = fmax(mx, pv[j]);
+  }
+  if (mx == 0.0) mn = mx = 1.0;  // all-padding block
+  pst[2 * k] = mn;
+  pst[2 * k + 1] = mx;
+}
 
 __global__ __launch_bounds__(256) void pivot_init_kernel(SpdBatch b) {
   const int m = blockIdx.x;
@@ -120,7 +135,10 @@ __global__ __launch_bounds__(256) void pivot_init_kernel(SpdBatch b) {
   const double ls = pivot_chol_inv_block(A, M, pv, t, b.status[m]);
   double* piv = b.piv[m];
   for (int e = t; e < 1024; e += 256) piv[e] = M[(e >> 5) * SP + (e & 31)];
-  if (t == 0) b.ldet[m][0] = ls;
+  if (t == 0) {
+    b.ldet[m][0] = ls;
+    write_pivot_stats(pv, 0, b.n[m], b.pst[m]);
+  }
 }
 
 // acc += A(32x32, element (i,k) at a[i*sai + k*sak]) * B(32x32, (k,j) at bm[k*sbk + j*sbj]),
@@ -221,7 +239,27 @@ __global__ __launch_bounds__(256) void sweep_kernel(SpdBatch b, int k) {
   const double ls = pivot_chol_inv_block(sP, sM, pv, t, b.status[m]);
   double* piv = b.piv[m] + (size_t)(k + 1) * 1024;
   for (int e = t; e < 1024; e += 256) piv[e] = sM[(e >> 5) * SP + (e & 31)];
-  if (t == 0) b.ldet[m][k + 1] = ls;
+  if (t == 0) {
+    b.ldet[m][k + 1] = ls;
+    write_pivot_stats(pv, k + 1, b.n[m], b.pst[m]);
+  }
+}
+
+// One launch of the inverse: stage -1 = pivot_init, stage k >= 0 = sweep k (bench/profiling).
+hipError_t launch_spd_stage(SpdArgs* a, int nmat, int stage, hipStream_t s) {
+  SpdBatch b{};
+  int Tmax = 0;
+  for (int m = 0; m < nmat; ++m) {
+    b.X[m] = a[m].X; b.Y[m] = a[m].Y; b.p[m] = a[m].p; b.T[m] = a[m].p / 32;
+    b.piv[m] = a[m].piv; b.ldet[m] = a[m].ldet; b.status[m] = a[m].status;
+    b.pst[m] = a[m].pst; b.n[m] = a[m].n;
+    if (b.T[m] > Tmax) Tmax = b.T[m];
+  }
+  if (stage < 0)
+    hipLaunchKernelGGL(pivot_init_kernel, dim3(nmat), dim3(256), 0, s, b);
+  else
+    hipLaunchKernelGGL(sweep_kernel, dim3(Tmax * Tmax, nmat), dim3(256), 0, s, b, stage);
+  return hipGetLastError();
 }
 
 hipError_t launch_spd_inverse(SpdArgs* a, int nmat, double** final_out, hipStream_t s) {
@@ -234,6 +272,8 @@ hipError_t launch_spd_inverse(SpdArgs* a, int nmat, double** final_out, hipStrea
     b.T[m] = a[m].p / 32;
     b.piv[m] = a[m].piv;
     b.ldet[m] = a[m].ldet;
+    b.pst[m] = a[m].pst;
+    b.n[m] = a[m].n;
     b.status[m] = a[m].status;
     if (b.T[m] > Tmax) Tmax = b.T[m];
     // sweep k reads (k even ? X : Y) and writes the other; T sweeps end in:

@@ -44,7 +44,8 @@ struct AdamUArgs {
   double llk_weight;
   int apply, ac;
   const StepScalars* sc;
-  const double* E1; const double* E2; const double* R;
+  // 2D: gU = S + v (X1 + X2) (X1 includes beta for advection); 1D: gu = X1 + v X2 (alpha, beta)
+  const double* S; const double* X1; const double* X2; const double* R;
   double* Up;
   const double* bvals;
   const int* bidx; int nb;

@@ -167,7 +167,7 @@ hipError_t launch_finalize(const FinalizeArgs& f, hipStream_t s) {
   return hipGetLastError();
 }
 
-// dL/dU and Adam on the solution grid.  2D: gU = E1 + E2 (= S + v(X1+X2))
+// dL/dU and Adam on the solution grid.  2D: gU = S + v(X1 + X2)
 //   [+ v(3U^2-1)R for Allen-Cahn] + w*tau*scatter(u_b - b);  1D: gu = alpha + v*beta [+...].
 __global__ __launch_bounds__(256) void adam_u_kernel(AdamUArgs A) {
   const Layout& L = A.L;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void adam_u_kernel(AdamUArgs A) {
     const int i = e / L.n2, j = e % L.n2;
     pi = (size_t)i * L.p2 + j;
     u = A.Up[pi];
-    g = A.E1[pi] + A.E2[pi];
+    g = A.S[pi] + v * (A.X1[pi] + A.X2[pi]);
     if (A.ac) g += v * (3.0 * u * u - 1.0) * A.R[pi];
     const int n1 = L.n1, n2 = L.n2;
     if (i == 0) g += wt * (u - A.bvals[j]);
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void adam_u_kernel(AdamUArgs A) {
   } else {
     pi = e;
     u = A.Up[pi];
-    g = A.E1[pi] + v * A.E2[pi];  // alpha + v*beta
+    g = A.X1[pi] + v * A.X2[pi];  // alpha + v*beta
     if (A.ac) g += v * (3.0 * u * u - 1.0) * A.R[pi];
     for (int k = 0; k < A.nb; ++k)
       if (A.bidx[k] == e) g += wt * (u - A.bvals[k]);

@@ -66,6 +66,10 @@ EXPORTS = {
     "gpk_profile_stages": ([ctypes.c_void_p, ctypes.c_int32, _dp, ctypes.c_int32, _ip], ctypes.c_int),
     "gpk_stage_name": ([ctypes.c_void_p, ctypes.c_int32], ctypes.c_char_p),
     "gpk_time_spd_inverse": ([ctypes.c_void_p, ctypes.c_int32, _dp], ctypes.c_int),
+    "gpk_bench_kernel": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32, _dp, _dp, _dp], ctypes.c_int),
+    "gpk_kernel_pairs": ([ctypes.c_int32, ctypes.c_int32, _dp, _dp, ctypes.c_int64, _dp, _dp, _dp,
+                          ctypes.c_int32, _dp], ctypes.c_int),
+    "gpk_forward_field": ([ctypes.c_void_p, ctypes.c_int32, _dp, ctypes.c_int64], ctypes.c_int),
 }
 
 _LIB = None

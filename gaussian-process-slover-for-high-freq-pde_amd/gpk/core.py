@@ -160,6 +160,22 @@ class DeviceSolver:
         check(_lib.load().gpk_criterion(self._h, ctypes.byref(c)))
         return c.value
 
+    FIELDS_2D = {"K1": 0, "K2": 1, "K1inv_U": 2, "K2inv_Ut": 3, "U_xx": 4, "U_yy": 5}
+    FIELDS_1D = {"K": 0, "Kinv_u": 2, "u_xx": 4}
+
+    def forward_field(self, name):
+        """value_and_grad_kernel quantities at the current params, computed on the device."""
+        if self.dim == 2:
+            what = self.FIELDS_2D[name]
+            shape = [(self.n1, self.n1), (self.n2, self.n2), (self.n1, self.n2),
+                     (self.n2, self.n1), (self.n1, self.n2), (self.n1, self.n2)][what]
+        else:
+            what = self.FIELDS_1D[name]
+            shape = (self.n1, self.n1) if what == 0 else (self.n1, 1)
+        out = np.empty(shape)
+        check(_lib.load().gpk_forward_field(self._h, what, dptr(out), out.size))
+        return out
+
     # -- measurement -----------------------------------------------------------------------
     def profile_stages(self, iters=10):
         lib = _lib.load()
@@ -173,6 +189,27 @@ class DeviceSolver:
         us = ctypes.c_double()
         check(_lib.load().gpk_time_spd_inverse(self._h, int(iters), ctypes.byref(us)))
         return us.value
+
+    def bench_kernel(self, name, iters=50):
+        """(avg_us, algorithmic_flops, algorithmic_bytes) of one kernel launch (HIP events)."""
+        us, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(_lib.load().gpk_bench_kernel(self._h, name.encode(), int(iters), ctypes.byref(us),
+                                           ctypes.byref(fl), ctypes.byref(by)))
+        return us.value, fl.value, by.value
+
+
+def kernel_pairs(kind, x1, x2, paras, deriv=0):
+    """gpk_kernel_pairs: elementwise kappa / D_x1_kappa / DD_x1_kappa over pairs (vmap)."""
+    lib = _lib.load()
+    a, b = f64(x1).reshape(-1), f64(x2).reshape(-1)
+    if a.size != b.size:
+        raise ValueError("x1 and x2 must have the same number of elements")
+    lw, ll, fr = (f64(paras[k]).reshape(-1) for k in ("log-w", "log-ls", "freq"))
+    out = np.empty(a.size)
+    k = _lib.KIND_IDS[kind] if isinstance(kind, str) else int(kind)
+    check(lib.gpk_kernel_pairs(k, int(deriv), dptr(a), dptr(b), a.size, dptr(lw), dptr(ll),
+                               dptr(fr), lw.size, dptr(out)))
+    return out
 
 
 def kernel_matrices(kind, x1, x2, paras, jitter=0.0, deriv=0):

@@ -90,6 +90,13 @@ int gpk_kernel_matrices(int32_t kind, int32_t deriv, const double* x1, int32_t n
                         const double* freq, int32_t q, double jitter, double* K_out,
                         double* D_out);
 
+/* vmap(kappa) / vmap(D_x1_kappa) / vmap(DD_x1_kappa) over n elementwise pairs
+ * (x1[e], x2[e]) -- the reference's per-pair kernel calls (kernel_matrix.py:26,
+ * model_GP_solver_2d.py:107-117): out[e] for deriv 0 / 1 / 2.  No jitter. */
+int gpk_kernel_pairs(int32_t kind, int32_t deriv, const double* x1, const double* x2, int64_t n,
+                     const double* logw, const double* logls, const double* freq, int32_t q,
+                     double* out);
+
 /* Solver object: copies the problem to device memory; params start at the reference init
  * (train(), model_GP_solver_2d.py:245-261 / model_GP_solver_1d.py:203-213) with zero Adam
  * state.  freq_scale sets the initial frequencies linspace(0,1,Q)*freq_scale. */
@@ -123,6 +130,13 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
 
 /* compute_early_stopping (model_GP_solver_2d.py:222-233): bgap/Nb + egap/Nc */
 int gpk_criterion(gpk_handle* h, double* out);
+
+/* value_and_grad_kernel (model_GP_solver_2d.py:87-121 / model_GP_solver_1d.py:80-99) at the
+ * current params, computed on the device; `what` selects one field, out gets it unpadded:
+ *   2D: 0 K1 [n1*n1], 1 K2 [n2*n2], 2 K1inv_U [n1*n2], 3 K2inv_Ut [n2*n1], 4 U_xx [n1*n2],
+ *       5 U_yy [n1*n2]   (advection: U_x, U_y)
+ *   1D: 0 K [n*n], 2 Kinv_u [n], 4 u_xx [n]                                                */
+int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n);
 
 /* Per-stage device timings (HIP events on the handle's stream) of one step, averaged over
  * `iters` eager (non-graph) steps run on a saved copy of the state: out_us[stage], names via

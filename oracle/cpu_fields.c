@@ -10,6 +10,11 @@
  * pure-NumPy statement this file is tested against in tests/test_oracle.py).  Dense linear
  * algebra of the CPU baseline stays in NumPy/SciPy (OpenBLAS LU), as in gp_oracle.py.
  *
+ * Performance structure (so the CPU baseline is a credible stand-in for JAX/XLA-CPU): rows
+ * are split over OpenMP threads; the inner loop runs over the columns j of a row with
+ * `omp simd`, so exp/sin/cos vectorise through glibc's libmvec (built with -ffast-math);
+ * square symmetric blocks evaluate only j <= i and mirror, exactly like the GPU path.
+ *
  * kind: 0 SE_Cos_1d, 1 Matern52_Cos_1d, 2 SE_1d, 3 Matern52_1d.
  */
 #include <math.h>
@@ -19,96 +24,159 @@
 #define SQRT5 2.23606797749978969641
 #define TWO_PI 6.28318530717958647692
 
-typedef struct {
-  double m0, m1, m2, m0l, m1l, m2l;
-} radial_t;
-typedef struct {
-  double c0, c1, c2, c0f, c1f, c2f;
-} cosine_t;
+static inline int is_matern(int k) { return k == 1 || k == 3; }
+static inline int has_cos(int k) { return k == 0 || k == 1; }
 
-static inline void radial(int kind, double d, double a, int want_l, radial_t* o) {
-  if (kind == 1 || kind == 3) { /* Matern52: r = sqrt5 a d (code/kernel_matrix.py:147-151) */
-    double r = SQRT5 * a * d, E = exp(-r);
-    double ka = SQRT5 * a / 3.0, k2 = 5.0 * a * a / 3.0;
-    o->m0 = (1.0 + r + r * r / 3.0) * E;
-    o->m1 = -ka * r * (1.0 + r) * E;
-    o->m2 = k2 * (r * r - r - 1.0) * E;
-    if (want_l) {
-      o->m0l = -(r * r / 3.0) * (1.0 + r) * E;
-      o->m1l = -ka * r * (2.0 + 2.0 * r - r * r) * E;
-      o->m2l = k2 * (-r * r * r + 5.0 * r * r - 2.0 * r - 2.0) * E;
+/* One row i of K (and D) over columns j in [0, jend): accumulate component q into kr/dr. */
+static inline __attribute__((always_inline)) void row_kd_t(const int mat, const int deriv, double xi,
+                                                            const double* x2, int jend, double w,
+                                                            double a, double om, double* kr,
+                                                            double* dr) {
+#pragma omp simd
+  for (int j = 0; j < jend; ++j) {
+    const double diff = xi - x2[j];
+    const double d = fabs(diff);
+    double m0, m1, m2;
+    if (mat) {
+      const double r = SQRT5 * a * d, E = exp(-r);
+      m0 = (1.0 + r + r * r * (1.0 / 3.0)) * E;
+      m1 = -(SQRT5 / 3.0) * a * r * (1.0 + r) * E;
+      m2 = (5.0 / 3.0) * a * a * (r * r - r - 1.0) * E;
+    } else {
+      const double g = exp(-a * d * d);
+      m0 = g;
+      m1 = -2.0 * a * d * g;
+      m2 = (4.0 * a * a * d * d - 2.0 * a) * g;
     }
-  } else { /* SE: exp(-d^2 e^{log-ls}) (code/kernel_matrix.py:125) */
-    double d2 = d * d, g = exp(-a * d2);
-    o->m0 = g;
-    o->m1 = -2.0 * a * d * g;
-    o->m2 = (4.0 * a * a * d2 - 2.0 * a) * g;
-    if (want_l) {
-      o->m0l = -a * d2 * g;
-      o->m1l = (-2.0 * a * d + 2.0 * a * a * d2 * d) * g;
-      o->m2l = (10.0 * a * a * d2 - 2.0 * a - 4.0 * a * a * a * d2 * d2) * g;
-    }
+    /* non-cosine kinds pass om = 0: cos = 1, sin = 0 exactly */
+    const double C = cos(om * d), S = sin(om * d);
+    const double c0 = C, c1 = -om * S, c2 = -om * om * C;
+    kr[j] += w * (m0 * c0);
+    if (deriv == 2) dr[j] += w * (m2 * c0 + 2.0 * m1 * c1 + m0 * c2);
+    if (deriv == 1) dr[j] += w * ((m1 * c0 + m0 * c1) * (diff >= 0.0 ? 1.0 : -1.0));
   }
 }
 
-static inline void cosine(int kind, double d, double f, int want_f, cosine_t* o) {
-  if (kind == 0 || kind == 1) { /* cos(2 pi f d) (code/kernel_matrix.py:127,153) */
-    double w = TWO_PI * f, C = cos(w * d), S = sin(w * d);
-    o->c0 = C;
-    o->c1 = -w * S;
-    o->c2 = -w * w * C;
-    if (want_f) {
-      o->c0f = -TWO_PI * d * S;
-      o->c1f = -TWO_PI * S - TWO_PI * w * d * C;
-      o->c2f = -2.0 * TWO_PI * w * C + TWO_PI * w * w * d * S;
-    }
+static void row_kd(int kind, int deriv, double xi, const double* x2, int jend, double w,
+                   double a, double f, double* kr, double* dr) {
+  const double om = has_cos(kind) ? TWO_PI * f : 0.0;
+  /* every (radial, deriv) combination gets its own branch-free simd loop */
+  if (is_matern(kind)) {
+    if (deriv == 2) row_kd_t(1, 2, xi, x2, jend, w, a, om, kr, dr);
+    else if (deriv == 1) row_kd_t(1, 1, xi, x2, jend, w, a, om, kr, dr);
+    else row_kd_t(1, 0, xi, x2, jend, w, a, om, kr, dr);
   } else {
-    o->c0 = 1.0;
-    o->c1 = o->c2 = o->c0f = o->c1f = o->c2f = 0.0;
+    if (deriv == 2) row_kd_t(0, 2, xi, x2, jend, w, a, om, kr, dr);
+    else if (deriv == 1) row_kd_t(0, 1, xi, x2, jend, w, a, om, kr, dr);
+    else row_kd_t(0, 0, xi, x2, jend, w, a, om, kr, dr);
   }
 }
 
 /* K[n1*n2] (kappa, + jitter on i==j when add_jitter) and, if D != NULL, the deriv-order
- * derivative block (1: D_x1_kappa, 2: DD_x1_kappa).  Row-major, x1 indexes rows. */
-void oracle_kd(int kind, int deriv, const double* x1, int n1, const double* x2, int n2,
-               const double* logw, const double* logls, const double* freq, int Q,
-               double jitter, int add_jitter, double* K, double* D) {
+ * derivative block (1: D_x1_kappa, 2: DD_x1_kappa).  Row-major, x1 indexes rows.
+ * symmetric != 0 asserts x1 == x2 (square block): only j <= i is evaluated, then mirrored. */
+void oracle_kd2(int kind, int deriv, const double* x1, int n1, const double* x2, int n2,
+                const double* logw, const double* logls, const double* freq, int Q,
+                double jitter, int add_jitter, int symmetric, double* K, double* D) {
   double* w = (double*)malloc(sizeof(double) * Q * 2);
   double* a = w + Q;
   for (int q = 0; q < Q; ++q) {
     w[q] = exp(logw[q]);
     a[q] = exp(logls[q]);
   }
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(dynamic, 8)
   for (int i = 0; i < n1; ++i) {
-    for (int j = 0; j < n2; ++j) {
-      double diff = x1[i] - x2[j];
-      double d = fabs(diff), s = diff >= 0.0 ? 1.0 : -1.0; /* JAX abs' (0) = +1 */
-      double k = 0.0, dv = 0.0;
-      for (int q = 0; q < Q; ++q) {
-        radial_t m;
-        cosine_t c;
-        radial(kind, d, a[q], 0, &m);
-        cosine(kind, d, freq[q], 0, &c);
-        k += w[q] * (m.m0 * c.c0);
-        if (deriv == 1)
-          dv += w[q] * (m.m1 * c.c0 + m.m0 * c.c1);
-        else if (deriv == 2)
-          dv += w[q] * (m.m2 * c.c0 + 2.0 * m.m1 * c.c1 + m.m0 * c.c2);
+    const int jend = symmetric ? i + 1 : n2;
+    double* kr = K + (size_t)i * n2;
+    double* dr = D ? D + (size_t)i * n2 : NULL;
+    double tmp[1];
+    memset(kr, 0, sizeof(double) * jend);
+    if (dr) memset(dr, 0, sizeof(double) * jend);
+    for (int q = 0; q < Q; ++q)
+      row_kd(kind, D ? deriv : 0, x1[i], x2, jend, w[q], a[q], freq[q], kr, dr ? dr : tmp);
+    if (add_jitter && i < n2) kr[i] += jitter;
+  }
+  if (symmetric) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n1; ++i)
+      for (int j = i + 1; j < n2; ++j) {
+        K[(size_t)i * n2 + j] = K[(size_t)j * n2 + i];
+        if (D) D[(size_t)i * n2 + j] = (deriv == 1) ? -D[(size_t)j * n2 + i] : D[(size_t)j * n2 + i];
       }
-      if (add_jitter && i == j) k += jitter;
-      K[(size_t)i * n2 + j] = k;
-      if (D) D[(size_t)i * n2 + j] = deriv == 1 ? dv * s : dv;
-    }
   }
   free(w);
 }
 
+/* legacy entry (full evaluation), kept for the tests */
+void oracle_kd(int kind, int deriv, const double* x1, int n1, const double* x2, int n2,
+               const double* logw, const double* logls, const double* freq, int Q,
+               double jitter, int add_jitter, double* K, double* D) {
+  oracle_kd2(kind, deriv, x1, n1, x2, n2, logw, logls, freq, Q, jitter, add_jitter, 0, K, D);
+}
+
+static inline __attribute__((always_inline)) void pg_row_t(const int mat, const int deriv, int jend,
+                                                            const double* dd, const double* wk,
+                                                            const double* wd, double aq, double om,
+                                                            double* osf, double* osl, double* osw) {
+  double sf = 0.0, sl = 0.0, sw = 0.0;
+#pragma omp simd reduction(+ : sf, sl, sw)
+  for (int j = 0; j < jend; ++j) {
+    const double d = dd[j];
+    double m0, m1, m2, m0l, m1l, m2l;
+    if (mat) {
+      const double r = SQRT5 * aq * d, E = exp(-r), r2 = r * r;
+      const double ka = (SQRT5 / 3.0) * aq, k2 = (5.0 / 3.0) * aq * aq;
+      m0 = (1.0 + r + r2 * (1.0 / 3.0)) * E;
+      m1 = -ka * r * (1.0 + r) * E;
+      m2 = k2 * (r2 - r - 1.0) * E;
+      m0l = -(r2 * (1.0 / 3.0)) * (1.0 + r) * E;
+      m1l = -ka * r * (2.0 + 2.0 * r - r2) * E;
+      m2l = k2 * (-r2 * r + 5.0 * r2 - 2.0 * r - 2.0) * E;
+    } else {
+      const double d2 = d * d, g = exp(-aq * d2);
+      m0 = g;
+      m1 = -2.0 * aq * d * g;
+      m2 = (4.0 * aq * aq * d2 - 2.0 * aq) * g;
+      m0l = -aq * d2 * g;
+      m1l = (-2.0 * aq * d + 2.0 * aq * aq * d2 * d) * g;
+      m2l = (10.0 * aq * aq * d2 - 2.0 * aq - 4.0 * aq * aq * aq * d2 * d2) * g;
+    }
+    /* non-cosine kinds pass om = 0: cos = 1, sin = 0; their freq gradient is zeroed later */
+    const double C = cos(om * d), S = sin(om * d);
+    const double c0 = C, c1 = -om * S, c2 = -om * om * C;
+    const double c0f = -TWO_PI * d * S;
+    const double c1f = -TWO_PI * S - TWO_PI * om * d * C;
+    const double c2f = -2.0 * TWO_PI * om * C + TWO_PI * om * om * d * S;
+    const double fw = m0 * c0, fl = m0l * c0, ff = m0 * c0f;
+    double dw, dl, df;
+    if (deriv == 2) {
+      dw = m2 * c0 + 2.0 * m1 * c1 + m0 * c2;
+      dl = m2l * c0 + 2.0 * m1l * c1 + m0l * c2;
+      df = m2 * c0f + 2.0 * m1 * c1f + m0 * c2f;
+    } else if (deriv == 1) {
+      dw = m1 * c0 + m0 * c1;
+      dl = m1l * c0 + m0l * c1;
+      df = m1 * c0f + m0 * c1f;
+    } else {
+      dw = dl = df = 0.0;
+    }
+    sw += wk[j] * fw + wd[j] * dw;
+    sl += wk[j] * fl + wd[j] * dl;
+    sf += wk[j] * ff + wd[j] * df;
+  }
+  *osf = sf;
+  *osl = sl;
+  *osw = sw;
+}
+
 /* out[0:Q] = dL/dfreq, out[Q:2Q] = dL/dlog-ls, out[2Q:3Q] = dL/dlog-w of
- *   sum_ij GK[i,j] K_ij(theta) + GD[i,j] D_ij(theta)   over an n x n block of x. */
+ *   sum_ij GK[i,j] K_ij(theta) + GD[i,j] D_ij(theta)   over an n x n block of x.
+ * Pairs j < i carry the mirror's weight (K, DD symmetric; D_x1 sign folded into the weight). */
 void oracle_param_grad(int kind, int deriv, const double* x, int n, const double* logw,
                        const double* logls, const double* freq, int Q, const double* GK,
                        const double* GD, double* out) {
+  const int mat = is_matern(kind), cs = has_cos(kind);
+  if (!GD) deriv = 0;
   double* w = (double*)malloc(sizeof(double) * Q * 2);
   double* a = w + Q;
   for (int q = 0; q < Q; ++q) {
@@ -119,43 +187,54 @@ void oracle_param_grad(int kind, int deriv, const double* x, int n, const double
 #pragma omp parallel
   {
     double* acc = (double*)calloc(3 * Q, sizeof(double));
-#pragma omp for schedule(static)
+    double* wk = (double*)malloc(sizeof(double) * n);
+    double* wd = (double*)malloc(sizeof(double) * n);
+    double* dd = (double*)malloc(sizeof(double) * n);
+#pragma omp for schedule(dynamic, 8)
     for (int i = 0; i < n; ++i) {
-      for (int j = 0; j < n; ++j) {
-        double diff = x[i] - x[j];
-        double d = fabs(diff), s = diff >= 0.0 ? 1.0 : -1.0;
-        double gk = GK[(size_t)i * n + j], gd = GD ? GD[(size_t)i * n + j] : 0.0;
-        for (int q = 0; q < Q; ++q) {
-          radial_t m;
-          cosine_t c;
-          radial(kind, d, a[q], 1, &m);
-          cosine(kind, d, freq[q], 1, &c);
-          double fw = gk * (m.m0 * c.c0), fl = gk * (m.m0l * c.c0), ff = gk * (m.m0 * c.c0f);
-          if (deriv == 2) {
-            fw += gd * (m.m2 * c.c0 + 2.0 * m.m1 * c.c1 + m.m0 * c.c2);
-            fl += gd * (m.m2l * c.c0 + 2.0 * m.m1l * c.c1 + m.m0l * c.c2);
-            ff += gd * (m.m2 * c.c0f + 2.0 * m.m1 * c.c1f + m.m0 * c.c2f);
-          } else if (deriv == 1) {
-            double gs = gd * s;
-            fw += gs * (m.m1 * c.c0 + m.m0 * c.c1);
-            fl += gs * (m.m1l * c.c0 + m.m0l * c.c1);
-            ff += gs * (m.m1 * c.c0f + m.m0 * c.c1f);
-          }
-          acc[q] += ff;
-          acc[Q + q] += fl;
-          acc[2 * Q + q] += fw;
+      /* weights of the unordered pairs (i, j), j <= i */
+      for (int j = 0; j <= i; ++j) {
+        const double diff = x[i] - x[j];
+        const double sij = diff >= 0.0 ? 1.0 : -1.0, sji = -diff >= 0.0 ? 1.0 : -1.0;
+        double gkij = GK[(size_t)i * n + j], gkji = GK[(size_t)j * n + i];
+        double gdij = GD ? GD[(size_t)i * n + j] : 0.0, gdji = GD ? GD[(size_t)j * n + i] : 0.0;
+        if (deriv == 1) {
+          gdij *= sij;
+          gdji *= sji;
         }
+        dd[j] = fabs(diff);
+        wk[j] = (j == i) ? gkij : gkij + gkji;
+        wd[j] = (j == i) ? gdij : gdij + gdji;
+      }
+      for (int q = 0; q < Q; ++q) {
+        const double aq = a[q], om = cs ? TWO_PI * freq[q] : 0.0;
+        double sf = 0.0, sl = 0.0, sw = 0.0;
+        if (mat) {
+          if (deriv == 2) pg_row_t(1, 2, i + 1, dd, wk, wd, aq, om, &sf, &sl, &sw);
+          else if (deriv == 1) pg_row_t(1, 1, i + 1, dd, wk, wd, aq, om, &sf, &sl, &sw);
+          else pg_row_t(1, 0, i + 1, dd, wk, wd, aq, om, &sf, &sl, &sw);
+        } else {
+          if (deriv == 2) pg_row_t(0, 2, i + 1, dd, wk, wd, aq, om, &sf, &sl, &sw);
+          else if (deriv == 1) pg_row_t(0, 1, i + 1, dd, wk, wd, aq, om, &sf, &sl, &sw);
+          else pg_row_t(0, 0, i + 1, dd, wk, wd, aq, om, &sf, &sl, &sw);
+        }
+        acc[q] += sf;
+        acc[Q + q] += sl;
+        acc[2 * Q + q] += sw;
       }
     }
 #pragma omp critical
     for (int t = 0; t < 3 * Q; ++t) out[t] += acc[t];
     free(acc);
+    free(wk);
+    free(wd);
+    free(dd);
   }
   for (int q = 0; q < Q; ++q) {
     out[q] *= w[q];
     out[Q + q] *= w[q];
     out[2 * Q + q] *= w[q];
-    if (!(kind == 0 || kind == 1)) out[q] = 0.0;
+    if (!cs) out[q] = 0.0;
   }
   free(w);
 }

@@ -52,6 +52,7 @@ def _clib():
         P = ctypes.POINTER(ctypes.c_double)
         i, d = ctypes.c_int, ctypes.c_double
         lib.oracle_kd.argtypes = [i, i, P, i, P, i, P, P, P, i, d, i, P, P]
+        lib.oracle_kd2.argtypes = [i, i, P, i, P, i, P, P, P, i, d, i, i, P, P]
         lib.oracle_param_grad.argtypes = [i, i, P, i, P, P, P, i, P, P, P]
         _CLIB = lib
     return _CLIB or None
@@ -177,6 +178,21 @@ def kernel_block(kind, x1, x2, paras, deriv=0):
     return out
 
 
+def kernel_kd(kind, x, paras, jitter, deriv):
+    """(K + jitter I, D) over the square block of x in one pass (C helper: symmetric, j <= i)."""
+    k = _kind_id(kind)
+    lib = _clib() if _USE_C else None
+    if lib is None:
+        return kernel_matrix(kind, x, paras, jitter), kernel_block(kind, x, x, paras, deriv)
+    xc = _c64(x)
+    lw, ll, fr = _c64(paras["log-w"]), _c64(paras["log-ls"]), _c64(paras["freq"])
+    K = np.empty((xc.size, xc.size))
+    D = np.empty_like(K)
+    lib.oracle_kd2(k, int(deriv), _ptr(xc), xc.size, _ptr(xc), xc.size, _ptr(lw), _ptr(ll),
+                   _ptr(fr), lw.size, float(jitter), 1, 1, _ptr(K), _ptr(D))
+    return K, D
+
+
 def kernel_matrix(kind, x, paras, jitter):
     """Kernel_matrix.get_kernel_matrix: vmap(kappa) + jitter*I (code/kernel_matrix.py:21-30)."""
     K = kernel_block(kind, x, x, paras, 0)
@@ -279,10 +295,9 @@ def loss_grad_1d(prob, params, want_grad=True):
     f = np.asarray(prob["src"], np.float64).reshape(-1)
     Nb = xind.size
 
-    K = kernel_matrix(kind, x, kp, prob["jitter"])          # :90
+    K, D = kernel_kd(kind, x, kp, prob["jitter"], 2)          # :90, :94-96
     lu = _lu(K)
     alpha = sla.lu_solve(lu, u)                                # :92
-    D = kernel_block(kind, x, x, kp, 2)                        # :94-96
     uxx = D @ alpha                                            # :97
     bres = u[xind] - yb
     bgap = float(bres @ bres)                                  # :105-106
@@ -385,13 +400,11 @@ def loss_grad_2d(prob, params, want_grad=True):
     deriv = 1 if eq == "advection" else 2
     beta = float(prob.get("beta", 1.0)) if eq == "advection" else 1.0
 
-    K1 = kernel_matrix(kind, x1, kp1, prob["jitter"])        # :97-99
-    K2 = kernel_matrix(kind, x2, kp2, prob["jitter"])        # :100-102
+    K1, D1 = kernel_kd(kind, x1, kp1, prob["jitter"], deriv)  # :97-99, :107-110
+    K2, D2 = kernel_kd(kind, x2, kp2, prob["jitter"], deriv)  # :100-102, :114-117
     lu1, lu2 = _lu(K1), _lu(K2)
     A = sla.lu_solve(lu1, U)                                  # :104  K1^{-1} U
     Bt = sla.lu_solve(lu2, U.T).T                             # :105  (K2^{-1} U^T)^T = U K2^{-1}
-    D1 = kernel_block(kind, x1, x1, kp1, deriv)               # :107-110
-    D2 = kernel_block(kind, x2, x2, kp2, deriv)               # :114-117
     Uxx = D1 @ A                                              # :112
     Uyy = Bt @ D2.T                                           # :119  (D2 K2^{-1} U^T)^T
     ub = boundary_2d(U)
@@ -412,12 +425,15 @@ def loss_grad_2d(prob, params, want_grad=True):
     loss = -(log_prior + log_b * wb + eq_ll)
     if not want_grad:
         return loss, None
-    # closed-form adjoints
+    # closed-form adjoints.  Every K^{-1} applied to a vector goes through
+    # the LU factors (backward stable, like JAX's solve transposes); the explicit inverse is
+    # only the log-det gradient term, as jnp.linalg.slogdet's backward rule forms it.  (An
+    # explicit-inverse product drifts by cond*eps*|K^-1||b|/|x|: 1.8e-5 in dL/dU at 400^2.)
     K1inv = sla.lu_solve(lu1, np.eye(N1))
     K2inv = sla.lu_solve(lu2, np.eye(N2))
-    S = A @ K2inv
-    X1 = K1inv @ (D1.T @ R) * beta
-    X2 = (R @ D2) @ K2inv
+    S = sla.lu_solve(lu2, A.T).T                              # K1^{-1} U K2^{-1}
+    X1 = sla.lu_solve(lu1, D1.T @ R) * beta                   # K1^{-1} D1^T R
+    X2 = sla.lu_solve(lu2, (R @ D2).T).T                      # R D2 K2^{-1}
     gU = S + v * (X1 + X2)
     if eq == "allencahn":
         gU = gU + v * (3.0 * U * U - 1.0) * R
