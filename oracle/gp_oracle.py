@@ -263,12 +263,60 @@ def param_grad_contract(kind, x, paras, GK, GD, deriv):
 # ----------------------------------------------------------------------------------------
 # LU helpers mirroring jnp.linalg.solve / slogdet (LAPACK getrf + getrs) [ext]
 # ----------------------------------------------------------------------------------------
+_EXTENDED = False
+
+
+def set_extended(flag):
+    """Extended-precision mode (x87 80-bit long double LU) for the solves / inverses / log-det:
+    an 'exact arithmetic' yardstick (eps 5.4e-20) for sizing the parity tolerances of
+    ill-conditioned cases.  Kernel fields and contractions stay fp64."""
+    global _EXTENDED
+    _EXTENDED = bool(flag)
+
+
+def _ext_lu(K):
+    A = np.array(K, dtype=np.longdouble)
+    n = A.shape[0]
+    perm = np.arange(n)
+    for k in range(n):
+        p = k + int(np.argmax(np.abs(A[k:, k])))
+        if p != k:
+            A[[k, p]] = A[[p, k]]
+            perm[[k, p]] = perm[[p, k]]
+        A[k + 1:, k] /= A[k, k]
+        A[k + 1:, k + 1:] -= np.outer(A[k + 1:, k], A[k, k + 1:])
+    return A, perm
+
+
+def _ext_solve(f, B):
+    A, perm = f
+    n = A.shape[0]
+    X = np.array(B, dtype=np.longdouble)[perm]
+    for k in range(n):                       # unit lower
+        X[k + 1:] -= np.multiply.outer(A[k + 1:, k], X[k])
+    for k in range(n - 1, -1, -1):           # upper
+        X[k] /= A[k, k]
+        X[:k] -= np.multiply.outer(A[:k, k], X[k])
+    return X.astype(np.float64)
+
+
 def _lu(K):
-    return sla.lu_factor(K, check_finite=False)
+    if _EXTENDED:
+        return ("ext", _ext_lu(K))
+    return ("lu", sla.lu_factor(K, check_finite=False))
 
 
-def _slogdet_from_lu(lu):
-    return float(np.sum(np.log(np.abs(np.diag(lu[0])))))
+def _solve(f, B):
+    """K^{-1} B through the factors (jnp.linalg.solve: LAPACK getrf + getrs)."""
+    if f[0] == "ext":
+        return _ext_solve(f[1], B)
+    return sla.lu_solve(f[1], B, check_finite=False)
+
+
+def _slogdet_from_lu(f):
+    d = np.diag(f[1][0])
+    return float(np.sum(np.log(np.abs(d.astype(np.float64)))) if f[0] == "lu" else
+                 np.sum(np.log(np.abs(d))))
 
 
 # ----------------------------------------------------------------------------------------
@@ -297,7 +345,7 @@ def loss_grad_1d(prob, params, want_grad=True):
 
     K, D = kernel_kd(kind, x, kp, prob["jitter"], 2)          # :90, :94-96
     lu = _lu(K)
-    alpha = sla.lu_solve(lu, u)                                # :92
+    alpha = _solve(lu, u)                                # :92
     uxx = D @ alpha                                            # :97
     bres = u[xind] - yb
     bgap = float(bres @ bres)                                  # :105-106
@@ -312,8 +360,8 @@ def loss_grad_1d(prob, params, want_grad=True):
     loss = -(log_prior + log_b * wb + eq_ll)                   # :148-149
     if not want_grad:
         return loss, None
-    beta = sla.lu_solve(lu, D.T @ R, trans=0)
-    Kinv = sla.lu_solve(lu, np.eye(N))
+    beta = _solve(lu, D.T @ R)
+    Kinv = _solve(lu, np.eye(N))
     GK = 0.5 * c * Kinv - 0.5 * np.outer(alpha, alpha) - v * np.outer(beta, alpha)
     GD = v * np.outer(R, alpha)
     gu = alpha + v * beta
@@ -336,7 +384,7 @@ def preds_1d(prob, params, xte):
     x = np.asarray(prob["x"], np.float64).reshape(-1)
     kp = params["kernel_paras"]
     K = kernel_matrix(kind, x, kp, prob["jitter"])
-    alpha = sla.lu_solve(_lu(K), np.asarray(params["u"], np.float64).reshape(-1))
+    alpha = _solve(_lu(K), np.asarray(params["u"], np.float64).reshape(-1))
     Kmn = kernel_block(kind, np.asarray(xte).reshape(-1), x, kp, 0)
     return Kmn @ alpha
 
@@ -348,7 +396,7 @@ def criterion_1d(prob, params):
     kp = params["kernel_paras"]
     u = np.asarray(params["u"], np.float64).reshape(-1)
     K = kernel_matrix(kind, x, kp, prob["jitter"])
-    alpha = sla.lu_solve(_lu(K), u)
+    alpha = _solve(_lu(K), u)
     uxx = kernel_block(kind, x, x, kp, 2) @ alpha
     xind = np.asarray(prob["xind"]).reshape(-1)
     bres = u[xind] - np.asarray(prob["y"]).reshape(-1)
@@ -403,8 +451,8 @@ def loss_grad_2d(prob, params, want_grad=True):
     K1, D1 = kernel_kd(kind, x1, kp1, prob["jitter"], deriv)  # :97-99, :107-110
     K2, D2 = kernel_kd(kind, x2, kp2, prob["jitter"], deriv)  # :100-102, :114-117
     lu1, lu2 = _lu(K1), _lu(K2)
-    A = sla.lu_solve(lu1, U)                                  # :104  K1^{-1} U
-    Bt = sla.lu_solve(lu2, U.T).T                             # :105  (K2^{-1} U^T)^T = U K2^{-1}
+    A = _solve(lu1, U)                                  # :104  K1^{-1} U
+    Bt = _solve(lu2, U.T).T                             # :105  (K2^{-1} U^T)^T = U K2^{-1}
     Uxx = D1 @ A                                              # :112
     Uyy = Bt @ D2.T                                           # :119  (D2 K2^{-1} U^T)^T
     ub = boundary_2d(U)
@@ -429,11 +477,11 @@ def loss_grad_2d(prob, params, want_grad=True):
     # the LU factors (backward stable, like JAX's solve transposes); the explicit inverse is
     # only the log-det gradient term, as jnp.linalg.slogdet's backward rule forms it.  (An
     # explicit-inverse product drifts by cond*eps*|K^-1||b|/|x|: 1.8e-5 in dL/dU at 400^2.)
-    K1inv = sla.lu_solve(lu1, np.eye(N1))
-    K2inv = sla.lu_solve(lu2, np.eye(N2))
-    S = sla.lu_solve(lu2, A.T).T                              # K1^{-1} U K2^{-1}
-    X1 = sla.lu_solve(lu1, D1.T @ R) * beta                   # K1^{-1} D1^T R
-    X2 = sla.lu_solve(lu2, (R @ D2).T).T                      # R D2 K2^{-1}
+    K1inv = _solve(lu1, np.eye(N1))
+    K2inv = _solve(lu2, np.eye(N2))
+    S = _solve(lu2, A.T).T                              # K1^{-1} U K2^{-1}
+    X1 = _solve(lu1, D1.T @ R) * beta                   # K1^{-1} D1^T R
+    X2 = _solve(lu2, (R @ D2).T).T                      # R D2 K2^{-1}
     gU = S + v * (X1 + X2)
     if eq == "allencahn":
         gU = gU + v * (3.0 * U * U - 1.0) * R
@@ -462,11 +510,11 @@ def preds_2d(prob, params, xte, yte):
     kp1, kp2 = params["kernel_paras_1"], params["kernel_paras_2"]
     U = np.asarray(params["U"], np.float64)
     K1 = kernel_matrix(kind, x1, kp1, prob["jitter"])
-    A = sla.lu_solve(_lu(K1), U)
+    A = _solve(_lu(K1), U)
     Kmn = kernel_block(kind, np.asarray(xte).reshape(-1), x1, kp1, 0)
     M1 = Kmn @ A
     K2 = kernel_matrix(kind, x2, kp2, prob["jitter"])
-    M2 = sla.lu_solve(_lu(K2), M1.T)
+    M2 = _solve(_lu(K2), M1.T)
     Kmn2 = kernel_block(kind, np.asarray(yte).reshape(-1), x2, kp2, 0)
     return (Kmn2 @ M2).T
 
@@ -480,8 +528,8 @@ def criterion_2d(prob, params):
     U = np.asarray(params["U"], np.float64)
     kp1, kp2 = params["kernel_paras_1"], params["kernel_paras_2"]
     deriv = 1 if eq == "advection" else 2
-    A = sla.lu_solve(_lu(kernel_matrix(kind, x1, kp1, prob["jitter"])), U)
-    Bt = sla.lu_solve(_lu(kernel_matrix(kind, x2, kp2, prob["jitter"])), U.T).T
+    A = _solve(_lu(kernel_matrix(kind, x1, kp1, prob["jitter"])), U)
+    Bt = _solve(_lu(kernel_matrix(kind, x2, kp2, prob["jitter"])), U.T).T
     Uxx = kernel_block(kind, x1, x1, kp1, deriv) @ A
     Uyy = Bt @ kernel_block(kind, x2, x2, kp2, deriv).T
     F = np.asarray(prob["src"]).reshape(U.shape)

@@ -2,7 +2,7 @@
 
 Tolerances (SURVEY.md §8(c) parity contract):
   K, D blocks             <= 1e-13 relative (max-abs / max)
-  loss, full gradient     <= max(1e-10, 50 cond(K) eps) relative (cond_tol)
+  loss, full gradient     <= max(1e-10, 50 cond(K) eps, 4 x oracle-vs-extended-precision error)
   predictions             <= 1e-10 relative
   short Adam trajectories <= 1e-9 relative
 """
@@ -63,22 +63,37 @@ def cond_tol(prob, params, floor=1e-10, factor=50.0):
     return max(floor, factor * c * np.finfo(np.float64).eps)
 
 
+def oracle_err(prob, params):
+    """Distance of the fp64 LU oracle (the reference's algorithm) from the same formulas
+    evaluated with extended-precision (80-bit) solves: its own rounding error, per key."""
+    fn = O.loss_grad_1d if "x" in prob else O.loss_grad_2d
+    lo, go = fn(prob, params)
+    O.set_extended(True)
+    try:
+        lt, gt = fn(prob, params)
+    finally:
+        O.set_extended(False)
+    errs = {k: rel(O.flatten_params(go[k]), O.flatten_params(gt[k])) for k in go}
+    errs["loss"] = abs(lo - lt) / abs(lt)
+    return lo, go, errs
+
+
 def _cmp_lossgrad(prob, params, Q, fs, tol=None):
+    """GPU vs oracle within max(cond_tol, 4 x the oracle's own distance from exact arithmetic):
+    at cond(K) ~ 1e5..1e7 the reference algorithm itself is only good to ~1e-9 (kernel-parameter
+    gradients through the explicit K^{-1} of slogdet's backward rule)."""
     tol = cond_tol(prob, params) if tol is None else tol
     s = device_solver(prob, Q, fs)
     s.set_params(params)
     loss, g = s.loss_grad()
-    if "x" in prob:
-        lo, go = O.loss_grad_1d(prob, params)
-    else:
-        lo, go = O.loss_grad_2d(prob, params)
+    lo, go, errs = oracle_err(prob, params)
     gflat = O.flatten_params(go)
-    assert abs(loss - lo) / abs(lo) < tol, (loss, lo)
+    assert abs(loss - lo) / abs(lo) < max(tol, 4 * errs["loss"]), (loss, lo)
     gd = O.unflatten_params(params, g)
     for key in sorted(go):
         a, b = O.flatten_params(gd[key]), O.flatten_params(go[key])
-        assert rel(a, b) < tol, (key, rel(a, b))
-    assert rel(g, gflat) < tol
+        assert rel(a, b) < max(tol, 4 * errs[key]), (key, rel(a, b), errs[key])
+    assert rel(g, gflat) < max(tol, 4 * max(errs.values()))
     s.close()
 
 
