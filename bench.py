@@ -32,34 +32,6 @@ METRIC = "log-joint iters/sec + fp64 Cholesky GFLOP/s, 2D Poisson 256^2, 1-8 GPU
 KERNEL_LAUNCHES = {"sweep": None, "gemm_B": 5, "pgrad": 1, "assemble": 1}  # per step (sweep: T)
 
 
-def dist_setup(n_gpus):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    return world, rank, local
-
-
-def barrier(world, local):
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier(device_ids=[local])
-
-
-def max_over_ranks(x, world, local):
-    if world == 1:
-        return x
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
 def cpu_baseline(config, seconds, max_steps=400):
     """The CPU oracle (oracle/gp_oracle.py: NumPy/SciPy LU + OpenMP C fields) on the same
     workload, bounded sample of `seconds` of work (test infrastructure; never the product)."""
@@ -110,17 +82,19 @@ def main():
     ap.add_argument("--kernel-iters", type=int, default=50)
     a = ap.parse_args()
 
-    world, rank, local = dist_setup(a.gpus)
+    from gpk import replicas
     from gpk.problems import CONFIGS, make_solver
+    ctx = replicas.init("nccl")
+    world, rank, local = ctx.world, ctx.rank, ctx.local
     cfg = CONFIGS[a.config]
     s = make_solver(a.config, seed=rank, device=local)
     s.step(a.warmup)                     # warm-up: graph capture + caches
-    barrier(world, local)
+    replicas.barrier(ctx)
     t0 = time.perf_counter()
     losses = s.step(a.steps)             # exactly K steps; returns after a device sync
     t1 = time.perf_counter()
-    barrier(world, local)
-    dt = max_over_ranks(t1 - t0, world, local)
+    replicas.barrier(ctx)
+    dt = replicas.max_over_ranks(t1 - t0, ctx)
     value = world * a.steps / dt
 
     # fp64 SPD factor+inverse rate: potrf + potri = n^3 flops per Kronecker factor
@@ -187,9 +161,7 @@ def main():
         }
         print(json.dumps(out), flush=True)
     s.close()
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    replicas.shutdown(ctx)
 
 
 if __name__ == "__main__":

@@ -208,7 +208,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
   } else {
     const int P = L.p1;
     // every K^{-1} application gets one step of iterative refinement x += K^{-1}(b - K x),
-    // gated on the pivot spread (gemv skips itself when K is well conditioned)
+    // gated on a cond(K) lower bound (gemv skips itself when K is well conditioned)
     GemvDesc g{};
     g.lda = P; g.p = P; g.rows = P; g.alpha = 1.0; g.ac = ac; g.F = h->F; g.U = h->Up;
     auto gemv = [&](const double* A, const double* x, double* y, double alpha, const double* C0,
@@ -298,7 +298,7 @@ static int build_descs(gpk_handle* h) {
   };
   // Every solve against K (JAX: LU solves, model_GP_solver_2d.py:104-105 and the reverse
   // pass) is X = K^{-1} B (MFMA) plus one refinement X += K^{-1}(B - K X), whose two GEMMs are
-  // gated on the factor's pivot spread (skipped when K is well conditioned, e.g. 256^2).
+  // gated on a lower bound of cond(K) (refine_gate_open) (skipped when K is well conditioned, e.g. 256^2).
   const int n1 = L.n1, n2 = L.n2;
   auto gate = [&](GemmDesc g, int axis) {
     g.gate = h->pst[axis];

@@ -107,16 +107,18 @@ struct SpdArgs {
   int n;           // true dim (pads are identity)
   double* piv;     // [(p/NB) * NB*NB] pivot-block inverse scratch
   double* ldet;    // [p/NB] logdet contribution of each pivot block
-  double* pst;     // [p/NB][2] min / max Cholesky pivot (L_ii^2) of each block
+  double* pst;     // refinement gate [p/NB + 1]: max diag K^{-1} per block, then K_00
   int* status;     // nonzero => not positive definite
 };
 // Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.
 hipError_t launch_spd_inverse(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
 hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
 
-// Iterative-refinement gate: a refinement GEMM/GEMV runs only when the factor's Cholesky
-// pivot spread max(L_ii^2)/min(L_ii^2) (a lower bound on cond(K)) exceeds this.
-constexpr double REFINE_PIVOT_RATIO = 100.0;
+// Iterative-refinement gate: a refinement GEMM/GEMV runs only when the factor's condition
+// number may exceed REFINE_COND_LB.  gate[0..ngate) = max diagonal of K^{-1} per 32-block,
+// gate[ngate] = K_00 = max diagonal of K; their product is a lower bound on cond_2(K)
+// (lambda_max >= max K_ii, 1/lambda_min >= max (K^{-1})_ii).
+constexpr double REFINE_COND_LB = 8.0;
 
 // Batched fp64 MFMA GEMM with fused epilogues.
 enum Epi {
@@ -138,7 +140,7 @@ struct GemmDesc {
   int vscale, vscale2;      // multiply alpha / alpha2 by v (StepScalars) when 1
   double* red;              // per-tile partial sums, [tiles] (nullable)
   double* red2; const double* Q1; const double* Q2;  // EPI_RESID: sum Q1*Q2 (quad term)
-  const double* gate; int ngate;  // pivot stats [ngate][2]; skip unless spread > ratio
+  const double* gate; int ngate;  // refinement gate (refine_gate_open); nullptr = always run
 };
 // small = 1: 16x16-tile latency kernel (max_tiles counts 16x16 tiles); 0: 32x32 LDS-tiled
 hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles,
@@ -148,12 +150,9 @@ inline bool gemm_use_small(long tiles16_total) { return tiles16_total <= 16384; 
 
 __device__ __forceinline__ bool refine_gate_open(const double* gate, int ngate) {
   if (!gate) return true;
-  double mn = gate[0], mx = gate[1];
-  for (int k = 1; k < ngate; ++k) {
-    mn = fmin(mn, gate[2 * k]);
-    mx = fmax(mx, gate[2 * k + 1]);
-  }
-  return mx > REFINE_PIVOT_RATIO * mn;
+  double mx = gate[0];
+  for (int k = 1; k < ngate; ++k) mx = fmax(mx, gate[k]);
+  return mx * gate[ngate] > REFINE_COND_LB;
 }
 
 // GEMV y = alpha * A x + beta * C0 (A padded, op N), optional epilogues like GEMM

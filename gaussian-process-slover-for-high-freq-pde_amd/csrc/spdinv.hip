@@ -106,23 +106,10 @@ struct SpdBatch {
   int T[2];       // p / 32
   double* piv[2]; // [T][32*32] L^{-1} of each pivot block
   double* ldet[2];
-  double* pst[2];  // [T][2] min / max pivot of each block (refinement gate)
-  int n[2];        // true size: pivots of padded rows (exactly 1) are left out of pst
+  double* pst[2];  // refinement gate: [0, T) max diag of K^{-1} per diagonal block, [T] = K_00
+  int n[2];        // true size: padded rows (identity) are left out of pst
   int* status[2];
 };
-
-// thread 0: min / max of the real (unpadded) pivots of block k
-__device__ __forceinline__ void write_pivot_stats(const double* pv, int k, int n, double* pst) {
-  double mn = 1.0e300, mx = 0.0;
-  for (int j = 0; j < 32; ++j) {
-    if (k * 32 + j >= n) break;
-    mn = fmin(mn, pv[j]);
-    mx = fmax(mx, pv[j]);
-  }
-  if (mx == 0.0) mn = mx = 1.0;  // all-padding block
-  pst[2 * k] = mn;
-  pst[2 * k + 1] = mx;
-}
 
 __global__ __launch_bounds__(256) void pivot_init_kernel(SpdBatch b) {
   const int m = blockIdx.x;
@@ -137,7 +124,7 @@ __global__ __launch_bounds__(256) void pivot_init_kernel(SpdBatch b) {
   for (int e = t; e < 1024; e += 256) piv[e] = M[(e >> 5) * SP + (e & 31)];
   if (t == 0) {
     b.ldet[m][0] = ls;
-    write_pivot_stats(pv, 0, b.n[m], b.pst[m]);
+    b.pst[m][b.T[m]] = X[0];  // K_00 = max diag K (stationary kernel + jitter)
   }
 }
 
@@ -233,16 +220,23 @@ __global__ __launch_bounds__(256) void sweep_kernel(SpdBatch b, int k) {
       y = xij[r] - acc[r];
     Y[o] = y * fin;
     if (nextpiv) sP[row * SP + col] = y;
+    if (last && I == J && row == col) pv[row] = (I * 32 + row < b.n[m]) ? y * fin : 0.0;
+  }
+  if (last && I == J) {  // block-uniform: refinement gate, max_i (K^{-1})_ii of this block
+    __syncthreads();
+    if (t == 0) {
+      double mx = 0.0;
+      for (int j = 0; j < 32; ++j) mx = fmax(mx, pv[j]);
+      b.pst[m][I] = mx;
+    }
+    return;
   }
   if (!nextpiv) return;  // block-uniform
   __syncthreads();
   const double ls = pivot_chol_inv_block(sP, sM, pv, t, b.status[m]);
   double* piv = b.piv[m] + (size_t)(k + 1) * 1024;
   for (int e = t; e < 1024; e += 256) piv[e] = sM[(e >> 5) * SP + (e & 31)];
-  if (t == 0) {
-    b.ldet[m][k + 1] = ls;
-    write_pivot_stats(pv, k + 1, b.n[m], b.pst[m]);
-  }
+  if (t == 0) b.ldet[m][k + 1] = ls;
 }
 
 // One launch of the inverse: stage -1 = pivot_init, stage k >= 0 = sweep k (bench/profiling).

@@ -8,7 +8,7 @@ import time
 import numpy as np
 
 from . import model_GP_solver_2d as m2d
-from . import utils
+from . import replicas, utils
 from .cli import parse_flags
 from .equations import EQUATIONS_1D, solution_1d
 from .infras.exp_config import ExpConfig
@@ -109,23 +109,31 @@ def test(trick_paras):
     Xind = np.array([0, X_col.shape[0] - 1])
     y = np.array([u(X_col[Xind[0]]), u(X_col[Xind[1]])]).reshape(-1)
     src_vals = get_source_val(src, X_col.reshape(-1))
-    err_list, early_stopping_list = [], []
+    # folds are independent problems: with WORLD_SIZE > 1 each rank trains its own folds on
+    # its own GPU (gpk/replicas.py); results are gathered in fold order
+    ctx = replicas.init()
+    if ctx.world > 1:
+        trick_paras = dict(trick_paras, device=ctx.local)
+    results = {}
     start_time = time.time()
     model = None
-    for fold in range(trick_paras["num_fold"]):
+    for fold in replicas.owned(trick_paras["num_fold"], ctx):
         print("fold %d training" % fold)
         model = GP_solver_1d_single(Xind, y, X_col, src_vals, 1e-6, X_test, Y_test, trick_paras)
         log_dict, early_stopping, min_err = model.train(trick_paras["nepoch"], fold)
-        err_list.append(min_err)
-        early_stopping_list.append(early_stopping["epoch"])
+        results[fold] = (min_err, early_stopping["epoch"])
         if fold == 0:
             utils.store_model(model, log_dict, trick_paras)
+    allres = replicas.gather_by_index(results, trick_paras["num_fold"], ctx)
+    err_list = [r[0] for r in allres]
+    early_stopping_list = [r[1] for r in allres]
     end_time = time.time()
     err_dict = {"mean": np.mean(err_list), "std": np.std(err_list), "err_list": err_list,
                 "stop_epoch_mean": np.mean(early_stopping_list), "used_time": end_time - start_time,
                 "avg_time": (end_time - start_time) / trick_paras["num_fold"]}
-    utils.wrirte_log(model, err_dict, trick_paras)
-    print("finish writing log ...")
+    if ctx.rank == 0:
+        utils.wrirte_log(model, err_dict, trick_paras)
+        print("finish writing log ...")
     return err_dict
 
 

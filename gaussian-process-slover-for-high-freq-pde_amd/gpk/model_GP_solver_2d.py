@@ -11,7 +11,7 @@ import time
 import numpy as np
 import yaml
 
-from . import init_func, utils
+from . import init_func, replicas, utils
 from .cli import parse_flags
 from .core import DeviceSolver  # noqa: F401  (re-export for users of the handle)
 from .equations import EQUATIONS_2D, boundary_2d, solution_2d
@@ -136,23 +136,31 @@ def test(trick_paras, solver_cls=None, beta=None):
     src_vals = get_source_val(src, x_pos_tr, y_pos_tr).reshape((x_pos_tr.size, y_pos_tr.size))
     X_test = (x_pos_test, y_pos_test)
     X_col = (x_pos_tr, y_pos_tr)
-    err_list, early_stopping_list = [], []
+    # folds are independent problems: with WORLD_SIZE > 1 each rank trains its own folds on
+    # its own GPU (gpk/replicas.py); results are gathered in fold order
+    ctx = replicas.init()
+    if ctx.world > 1:
+        trick_paras = dict(trick_paras, device=ctx.local)
+    results = {}
     start_time = time.time()
     model = None
-    for fold in range(trick_paras["num_fold"]):
+    for fold in replicas.owned(trick_paras["num_fold"], ctx):
         print("fold %d training" % fold)
         model = solver_cls(bvals, X_col, src_vals, 1e-6, X_test, u_test_mh, trick_paras)
         log_dict, early_stopping, min_err = model.train(trick_paras["nepoch"], fold)
-        err_list.append(min_err)
-        early_stopping_list.append(early_stopping["epoch"])
+        results[fold] = (min_err, early_stopping["epoch"])
         if fold == 0:
             utils.store_model(model, log_dict, trick_paras)
+    allres = replicas.gather_by_index(results, trick_paras["num_fold"], ctx)
+    err_list = [r[0] for r in allres]
+    early_stopping_list = [r[1] for r in allres]
     end_time = time.time()
     err_dict = {"mean": np.mean(err_list), "std": np.std(err_list), "err_list": err_list,
                 "stop_epoch_mean": np.mean(early_stopping_list), "used_time": end_time - start_time,
                 "avg_time": (end_time - start_time) / trick_paras["num_fold"]}
-    utils.wrirte_log(model, err_dict, trick_paras)
-    print("finish writing log ...")
+    if ctx.rank == 0:
+        utils.wrirte_log(model, err_dict, trick_paras)
+        print("finish writing log ...")
     return err_dict
 
 

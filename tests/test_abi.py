@@ -1,0 +1,101 @@
+"""C-ABI checks that need no GPU: libgpk.so loads, exports every include/gpk.h entry point, the
+ctypes mirror of gpk_problem has the C layout, and the product path refuses to run without a
+device (no CPU fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "gpk.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    return sorted(set(re.findall(r"\b(gpk_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    names = header_functions()
+    for must in ["gpk_kernel_matrices", "gpk_create", "gpk_step", "gpk_loss_grad", "gpk_set_params",
+                 "gpk_get_params", "gpk_predict", "gpk_criterion", "gpk_last_error", "gpk_destroy"]:
+        assert must in names
+
+
+def test_library_exports_every_header_symbol():
+    from gpk import _lib
+    lib = _lib.load()
+    missing = [n for n in header_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes table covers the same set (no stale or unbound entry points)
+    assert sorted(_lib.EXPORTS) == header_functions()
+
+
+def test_exports_are_c_symbols():
+    nm = subprocess.run(["nm", "-D", "--defined-only", os.path.join(
+        ROOT, "gaussian-process-slover-for-high-freq-pde_amd", "gpk", "_lib", "libgpk.so")],
+        capture_output=True, text=True, check=True).stdout
+    syms = {l.split()[-1] for l in nm.splitlines() if " T " in l}
+    for n in header_functions():
+        assert n in syms, f"{n} not exported with C linkage"
+
+
+def test_library_is_gfx950_code_object():
+    so = os.path.join(ROOT, "gaussian-process-slover-for-high-freq-pde_amd", "gpk", "_lib", "libgpk.so")
+    blob = open(so, "rb").read()
+    targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}, targets  # gfx950 code objects only, nothing else bundled
+
+
+def test_problem_struct_layout_matches_header(tmp_path):
+    """Compile a probe against include/gpk.h with gcc and compare sizeof/offsetof with ctypes."""
+    from gpk._lib import gpk_problem
+    fields = [f for f, _ in gpk_problem._fields_]
+    probe = tmp_path / "probe.c"
+    body = "\n".join(f'printf("{f} %zu\\n", offsetof(gpk_problem, {f}));' for f in fields)
+    probe.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gpk.h"\nint main(void){\n'
+                     'printf("sizeof %zu\\n", sizeof(gpk_problem));\n' + body + "\nreturn 0;}\n")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(probe), "-o", str(exe)],
+                   check=True)
+    out = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                 check=True).stdout.splitlines())
+    assert int(out["sizeof"]) == ctypes.sizeof(gpk_problem)
+    for f in fields:
+        assert int(out[f]) == getattr(gpk_problem, f).offset, f
+
+
+def test_abi_version_and_error_channel():
+    from gpk import _lib
+    lib = _lib.load()
+    assert lib.gpk_abi_version() == 1
+    assert isinstance(lib.gpk_last_error(), bytes)
+    # argument validation happens before any device work
+    rc = lib.gpk_create(None, 20.0, None)
+    assert rc == _lib.GPK_EINVAL
+    assert len(lib.gpk_last_error()) > 0
+    assert lib.gpk_destroy(None) in (_lib.GPK_OK, _lib.GPK_EINVAL)
+
+
+def test_no_cpu_fallback_without_device():
+    """On a host with no gfx950 device the product path raises instead of computing."""
+    from gpk import _lib
+    lib = _lib.load()
+    n = ctypes.c_int32(-1)
+    assert lib.gpk_device_count(ctypes.byref(n)) == _lib.GPK_OK
+    if n.value > 0:
+        pytest.skip("a device is visible")
+    from gpk.core import DeviceSolver, kernel_matrices
+    x = np.linspace(0, 1, 8)
+    with pytest.raises(_lib.GPKError):
+        DeviceSolver(1, "poisson", "Matern52_1d", x, np.zeros(8), np.zeros(2),
+                     bidx=np.array([0, 7], np.int32), Q=3)
+    kp = {"log-w": np.zeros(3), "log-ls": np.zeros(3), "freq": np.zeros(3)}
+    with pytest.raises(_lib.GPKError):
+        kernel_matrices("Matern52_1d", x, x, kp, 0.0, 2)
