@@ -96,13 +96,13 @@ __device__ __forceinline__ double epi_apply(const GemmDesc& d, double c, const E
   return c;
 }
 
-__global__ __launch_bounds__(256) void gemm_kernel(const GemmDesc* __restrict__ descs,
+__global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch,
                                                    const StepScalars* __restrict__ sc) {
-  const GemmDesc& d = descs[blockIdx.y];
+  const GemmDesc& d = batch.d[blockIdx.y];
   const int tn = d.N >> 5;
   const int tiles = (d.M >> 5) * tn;
   if ((int)blockIdx.x >= tiles) return;
-  if (!refine_gate_open(d.gate, d.ngate)) return;  // refinement not needed (uniform)
+  if (!gate_open(d.gate)) return;  // refinement not needed (uniform)
   const int ti = blockIdx.x / tn, tj = blockIdx.x % tn;
   const int i0 = ti * 32, j0 = tj * 32;
 
@@ -190,13 +190,15 @@ __device__ __forceinline__ d4 mma_chunk(const double* __restrict__ A, int lda, i
   return acc;
 }
 
-__global__ __launch_bounds__(256) void gemm_small_kernel(const GemmDesc* __restrict__ descs,
+__global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
                                                          const StepScalars* __restrict__ sc) {
-  const GemmDesc& d = descs[blockIdx.y];
+  const GemmDesc& d = batch.d[blockIdx.y];
   const int tn = d.N >> 4;
   const int tiles = (d.M >> 4) * tn;
   if ((int)blockIdx.x >= tiles) return;
-  if (!refine_gate_open(d.gate, d.ngate)) return;  // refinement not needed (uniform)
+  // the refinement gate is only consulted before the stores, so its load overlaps the operand
+  // loads instead of adding a dependent round trip (a closed gate wastes a few us of MFMA)
+  const bool open = gate_open(d.gate);
   const int i0 = (blockIdx.x / tn) * 16, j0 = (blockIdx.x % tn) * 16;
   __shared__ double part[2][4][256];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmDesc* __restr
     part[1][wv][lane * 4 + r] = acc2[r];
   }
   __syncthreads();
-  if (wv != 0) return;
+  if (wv != 0 || !open) return;
   double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
   if (d.vscale2) alpha2 *= sc->v;
@@ -252,12 +254,15 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(const GemmDesc* __restr
   }
 }
 
-hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles,
+hipError_t launch_gemm_batch(const GemmDesc* descs, int ndesc, int max_tiles,
                              const StepScalars* sc, hipStream_t s, int small) {
+  if (ndesc < 1 || ndesc > GEMM_MAX_BATCH) return hipErrorInvalidValue;
+  GemmBatch b{};
+  for (int i = 0; i < ndesc; ++i) b.d[i] = descs[i];
   if (small)
-    hipLaunchKernelGGL(gemm_small_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, descs_dev, sc);
+    hipLaunchKernelGGL(gemm_small_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, b, sc);
   else
-    hipLaunchKernelGGL(gemm_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, descs_dev, sc);
+    hipLaunchKernelGGL(gemm_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, b, sc);
   return hipGetLastError();
 }
 
@@ -265,7 +270,7 @@ hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles
 // GEMV (1D solver, code/model_GP_solver_1d.py:92,97): one wave per row, 4 rows per block.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void gemv_kernel(GemvDesc d) {
-  if (!refine_gate_open(d.gate, d.ngate)) return;  // refinement not needed (uniform)
+  const bool open = gate_open(d.gate);  // consulted before the stores only
   __shared__ double sred[4], sred2[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int row = blockIdx.x * 4 + wv;
@@ -291,7 +296,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvDesc d) {
       part = y * d.U[row];
     }
     if (d.red2) part2 = d.Q1[row] * d.Q2[row];
-    d.y[row] = y;
+    if (open) d.y[row] = y;
   }
   if (d.red || d.red2) {
     if (lane == 0) {

@@ -97,7 +97,7 @@ struct gpk_handle {
   int nquad = 0, negap = 0;
   double *pgpart = nullptr, *pg = nullptr;
   int bpa = 0;
-  GemmDesc* descs = nullptr;
+  std::vector<GemmDesc> hdescs;  // per-stage GEMM descriptors (kernel arguments)
   Stage st[kGemmStages];
   double *Kc[2] = {}, *pst[2] = {};  // kept K (refinement residuals), pivot stats (gate)
   double* rvec = nullptr;            // 1D refinement residual
@@ -187,7 +187,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
   const int ac = h->prob.eq == GPK_ALLENCAHN;
   if (L.dim == 2) {
     for (int k = 0; k < kGemmStages; ++k) {
-      TRY(check_launch(launch_gemm_batch(h->descs + h->st[k].off, h->st[k].n, h->st[k].maxtiles,
+      TRY(check_launch(launch_gemm_batch(h->hdescs.data() + h->st[k].off, h->st[k].n, h->st[k].maxtiles,
                                          h->sc, h->s, h->st[k].small), "gemm"));
       mark(h, stage++);
     }
@@ -215,7 +215,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
                     double beta, int epi, double* red, bool gated) -> int {
       GemvDesc q = g;
       q.A = A; q.x = x; q.y = y; q.alpha = alpha; q.C0 = C0; q.beta = beta; q.epi = epi; q.red = red;
-      q.gate = gated ? h->pst[0] : nullptr; q.ngate = h->nldet[0];
+      q.gate = gated ? h->pst[0] : nullptr;
       TRY(check_launch(launch_gemv(q, h->s), "gemv"));
       mark(h, stage++);
       return GPK_OK;
@@ -302,7 +302,6 @@ static int build_descs(gpk_handle* h) {
   const int n1 = L.n1, n2 = L.n2;
   auto gate = [&](GemmDesc g, int axis) {
     g.gate = h->pst[axis];
-    g.ngate = h->nldet[axis];
     return g;
   };
   // Stage A: A = K1^{-1} U, Bt = U K2^{-1}                       (2d.py:104-105)
@@ -416,9 +415,9 @@ static int build_descs(gpk_handle* h) {
   }
   end(10);
   h->nquad = h->negap = h->st[3].small ? (P1 / 16) * (P2 / 16) : (P1 / 32) * (P2 / 32);
-  TRY(h->alloc(&h->descs, d.size()));
-  HIPCHK(hipMemcpyAsync(h->descs, d.data(), d.size() * sizeof(GemmDesc), hipMemcpyHostToDevice, h->s));
-  HIPCHK(hipStreamSynchronize(h->s));
+  for (int k = 0; k < kGemmStages; ++k)
+    if (h->st[k].n > GEMM_MAX_BATCH) return fail(GPK_EINVAL, "internal: GEMM stage batch too large");
+  h->hdescs = d;
   return GPK_OK;
 }
 
@@ -635,7 +634,7 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
     A_(h->piv[a], (size_t)P * 32);
     A_(h->ldet[a], P / 32);
     A_(h->Kc[a], (size_t)P * P);
-    A_(h->pst[a], 2 * (P / 32));
+    A_(h->pst[a], 2);
     h->nldet[a] = P / 32;
   }
   if (L.dim == 2) {
@@ -873,14 +872,10 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
     d[5].beta = 1.0; d[5].C0 = Sw; d[5].ldc0 = P2;
     mk(d[6], Kmn1, P1, 0, Sw, P2, 0, Mw, P2, M1p, P2, P1);
     mk(d[7], Mw, P2, 0, Kmn2, P2, 1, res, M2p, M1p, M2p, P2);
-    GemmDesc* dd;
-    if (hipMalloc(&dd, sizeof(d)) != hipSuccess) { cleanup(); return fail(GPK_ENOMEM, "hipMalloc"); }
-    tmp.push_back(dd);
-    (void)hipMemcpyAsync(dd, d, sizeof(d), hipMemcpyHostToDevice, h->s);
     for (int k = 0; k < 8; ++k) {
       const long t16 = (long)(d[k].M / 16) * (d[k].N / 16);
       const int small = gemm_use_small(t16) ? 1 : 0;
-      (void)launch_gemm_batch(dd + k, 1, small ? (int)t16 : (d[k].M / 32) * (d[k].N / 32), h->sc, h->s, small);
+      (void)launch_gemm_batch(d + k, 1, small ? (int)t16 : (d[k].M / 32) * (d[k].N / 32), h->sc, h->s, small);
     }
     for (int i = 0; i < m1; ++i)
       (void)hipMemcpyAsync(out + (size_t)i * m2, res + (size_t)i * M2p, m2 * sizeof(double),
@@ -1062,7 +1057,7 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
   const int P1 = L.p1, P2 = L.p2;
   const double* src = (what == 3) ? h->Bt : h->A;
   if (what >= 4) {  // U_xx = D1 A  /  U_yy = Bt D2^T
-    HIPCHK(hipMalloc(&tmp, (size_t)P1 * P2 * sizeof(double) + sizeof(GemmDesc)));
+    HIPCHK(hipMalloc(&tmp, (size_t)P1 * P2 * sizeof(double)));
     GemmDesc g{};
     if (what == 4) {
       g.A = h->D[0]; g.lda = P1; g.B = h->A; g.ldb = P2; g.K = P1;
@@ -1070,12 +1065,9 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
       g.A = h->Bt; g.lda = P2; g.B = h->D[1]; g.ldb = P2; g.tb = 1; g.K = P2;
     }
     g.C = tmp; g.ldc = P2; g.M = P1; g.N = P2; g.alpha = 1.0; g.epi = EPI_STORE;
-    GemmDesc* dd = reinterpret_cast<GemmDesc*>(tmp + (size_t)P1 * P2);
-    hipError_t e = hipMemcpyAsync(dd, &g, sizeof(g), hipMemcpyHostToDevice, h->s);
     const long t16 = (long)(P1 / 16) * (P2 / 16);
     const int small = gemm_use_small(t16) ? 1 : 0;
-    if (e == hipSuccess)
-      e = launch_gemm_batch(dd, 1, small ? (int)t16 : (P1 / 32) * (P2 / 32), h->sc, h->s, small);
+    hipError_t e = launch_gemm_batch(&g, 1, small ? (int)t16 : (P1 / 32) * (P2 / 32), h->sc, h->s, small);
     if (e != hipSuccess) { cleanup(); return fail(GPK_EHIP, hipGetErrorString(e)); }
     src = tmp;
   }
@@ -1137,7 +1129,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     for (int a = 0; a < L.naxes; ++a) { const double n = a == 0 ? n1 : n2; bytes += 16.0 * n * n; }
   } else if (nm == "gemm_B" && L.dim == 2) {
     launch = [&]() {
-      return launch_gemm_batch(h->descs + h->st[3].off, h->st[3].n, h->st[3].maxtiles, h->sc, h->s,
+      return launch_gemm_batch(h->hdescs.data() + h->st[3].off, h->st[3].n, h->st[3].maxtiles, h->sc, h->s,
                                h->st[3].small);
     };
     // S = A K2^{-1} (2 n1 n2^2); R = D1 A + Bt D2^T (2 n1^2 n2 + 2 n1 n2^2)

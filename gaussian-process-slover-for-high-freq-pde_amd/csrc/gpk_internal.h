@@ -107,17 +107,17 @@ struct SpdArgs {
   int n;           // true dim (pads are identity)
   double* piv;     // [(p/NB) * NB*NB] pivot-block inverse scratch
   double* ldet;    // [p/NB] logdet contribution of each pivot block
-  double* pst;     // refinement gate [p/NB + 1]: max diag K^{-1} per block, then K_00
+  double* pst;     // refinement gate [2]: K_00, bits of max diag K^{-1} (gate_open)
   int* status;     // nonzero => not positive definite
 };
 // Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.
 hipError_t launch_spd_inverse(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
 hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
 
-// Iterative-refinement gate: a refinement GEMM/GEMV runs only when the factor's condition
-// number may exceed REFINE_COND_LB.  gate[0..ngate) = max diagonal of K^{-1} per 32-block,
-// gate[ngate] = K_00 = max diagonal of K; their product is a lower bound on cond_2(K)
-// (lambda_max >= max K_ii, 1/lambda_min >= max (K^{-1})_ii).
+// Iterative-refinement gate: a refinement GEMM/GEMV stores its result only when the factor's
+// condition number may exceed REFINE_COND_LB.  gate[0] = K_00 = max diagonal of K (written by
+// pivot_init), gate[1] = bit pattern of max_i (K^{-1})_ii (atomicMax by the last sweep); their
+// product is a lower bound on cond_2(K) (lambda_max >= max K_ii, 1/lambda_min >= max K^{-1}_ii).
 constexpr double REFINE_COND_LB = 8.0;
 
 // Batched fp64 MFMA GEMM with fused epilogues.
@@ -140,19 +140,24 @@ struct GemmDesc {
   int vscale, vscale2;      // multiply alpha / alpha2 by v (StepScalars) when 1
   double* red;              // per-tile partial sums, [tiles] (nullable)
   double* red2; const double* Q1; const double* Q2;  // EPI_RESID: sum Q1*Q2 (quad term)
-  const double* gate; int ngate;  // refinement gate (refine_gate_open); nullptr = always run
+  const double* gate; int ngate;  // refinement gate (gate_open); nullptr = always store
 };
-// small = 1: 16x16-tile latency kernel (max_tiles counts 16x16 tiles); 0: 32x32 LDS-tiled
-hipError_t launch_gemm_batch(const GemmDesc* descs_dev, int ndesc, int max_tiles,
+constexpr int GEMM_MAX_BATCH = 4;
+struct GemmBatch {  // passed by value (kernarg): no dependent descriptor load before the operands
+  GemmDesc d[GEMM_MAX_BATCH];
+};
+// small = 1: 16x16-tile latency kernel (max_tiles counts 16x16 tiles); 0: 32x32 LDS-tiled.
+// descs: HOST array of ndesc <= GEMM_MAX_BATCH descriptors (copied into the kernel arguments).
+hipError_t launch_gemm_batch(const GemmDesc* descs, int ndesc, int max_tiles,
                              const StepScalars* sc, hipStream_t s, int small);
 // heuristic: use the 16x16 latency kernel while the whole stage has few enough tiles
 inline bool gemm_use_small(long tiles16_total) { return tiles16_total <= 16384; }
 
-__device__ __forceinline__ bool refine_gate_open(const double* gate, int ngate) {
+__device__ __forceinline__ bool gate_open(const double* gate) {
   if (!gate) return true;
-  double mx = gate[0];
-  for (int k = 1; k < ngate; ++k) mx = fmax(mx, gate[k]);
-  return mx * gate[ngate] > REFINE_COND_LB;
+  const double k00 = gate[0];
+  const double mx = __longlong_as_double(*reinterpret_cast<const long long*>(gate + 1));
+  return mx * k00 > REFINE_COND_LB;
 }
 
 // GEMV y = alpha * A x + beta * C0 (A padded, op N), optional epilogues like GEMM

@@ -106,7 +106,7 @@ struct SpdBatch {
   int T[2];       // p / 32
   double* piv[2]; // [T][32*32] L^{-1} of each pivot block
   double* ldet[2];
-  double* pst[2];  // refinement gate: [0, T) max diag of K^{-1} per diagonal block, [T] = K_00
+  double* pst[2];  // refinement gate [2]: K_00, bits of max diag K^{-1} (gate_open)
   int n[2];        // true size: padded rows (identity) are left out of pst
   int* status[2];
 };
@@ -124,7 +124,8 @@ __global__ __launch_bounds__(256) void pivot_init_kernel(SpdBatch b) {
   for (int e = t; e < 1024; e += 256) piv[e] = M[(e >> 5) * SP + (e & 31)];
   if (t == 0) {
     b.ldet[m][0] = ls;
-    b.pst[m][b.T[m]] = X[0];  // K_00 = max diag K (stationary kernel + jitter)
+    b.pst[m][0] = X[0];  // K_00 = max diag K (stationary kernel + jitter)
+    b.pst[m][1] = 0.0;   // max diag K^{-1}: atomicMax'd by the last sweep
   }
 }
 
@@ -227,7 +228,9 @@ __global__ __launch_bounds__(256) void sweep_kernel(SpdBatch b, int k) {
     if (t == 0) {
       double mx = 0.0;
       for (int j = 0; j < 32; ++j) mx = fmax(mx, pv[j]);
-      b.pst[m][I] = mx;
+      // positive doubles order like their bit patterns
+      atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
+                (unsigned long long)__double_as_longlong(mx));
     }
     return;
   }
