@@ -14,6 +14,7 @@
 // sit in LDS.  Pads (i or j >= n) are written as identity (K) / zero (D) so the padded SPD
 // inverse stays block-diagonal.
 #include "gpk_internal.h"
+#include "spd_pivot.h"
 
 namespace gpk {
 
@@ -52,37 +53,94 @@ __device__ __forceinline__ void eval_kd(double diff, const double* w, const doub
   if (DERIV == 1 && !(diff >= 0.0)) D = -D;
 }
 
+constexpr int ASM_SUB = 16;  // workgroups per 32x32 tile: 64 elements (2 rows) each
+
 struct AssembleBatch {
   AssembleArgs ax[2];
   int tiles[2];   // lower-triangle tile count per axis
+  int pivot_x;    // blockIdx.x of the pivot-0 workgroup (per axis), or -1
+  PrepArgs prep;
 };
 
-constexpr int ASM_SUB = 16;  // workgroups per 32x32 tile: 64 elements (2 rows) each
+// exp of the params -> axis constants of component c (prep2 semantics, bitwise)
+__device__ __forceinline__ void axis_component(const PrepArgs& P, int axis, int q, int c, double& w,
+                                               double& a, double& om) {
+  const int off = P.off_kp[axis];
+  om = TWO_PI * P.params[off + c];          // freq
+  a = exp(P.params[off + q + c]);           // log-ls
+  w = exp(P.params[off + 2 * q + c]);       // log-w
+}
 
-// grid.x = lower-triangle tile * 16 + sub-block, grid.y = axis.  Thread t: element
-// e = t&63 of the sub-block (row 2*sub + (e>>5), col e&31), component group g = t>>6
-// (components g, g+4, ...).  The 4 partial sums are added in fixed order through LDS and
-// wave 0 writes the element and its mirror (K symmetric, DD symmetric, D_x1 antisymmetric).
+// workgroup (0, 0): publish the step constants for the later kernels of the step
+__device__ void publish_prep(const PrepArgs& P, int q) {
+  const int t = threadIdx.x;
+  for (int ax = 0; ax < P.naxes; ++ax)
+    for (int c = t; c < q; c += blockDim.x) {
+      double w, a, om;
+      axis_component(P, ax, q, c, w, a, om);
+      P.kc[ax].om[c] = om;
+      P.kc[ax].a[c] = a;
+      P.kc[ax].w[c] = w;
+    }
+  if (t == 0) {
+    P.sc->tau = exp(P.params[P.off_tau]);
+    P.sc->v = exp(P.params[P.off_v]);
+    const int n = *P.count + 1;
+    if (P.apply) *P.count = n;
+    P.sc->bc1 = 1.0 - pow(P.b1, (double)n);
+    P.sc->bc2 = 1.0 - pow(P.b2, (double)n);
+  }
+}
+
+// Pivot block 0 (rows/cols 0..31) of the SPD inverse, factored inside the assembly launch by
+// one extra workgroup per axis.  The 16 workgroups that assemble tile (0,0) release their rows
+// (agent-scope fence, then a counter increment); the pivot workgroup waits for all 16, acquires,
+// reads the tile and runs the Cholesky + L^{-1} of pivot_init.  It is dispatched after those
+// 16 (highest blockIdx.x), so they are resident or done: no deadlock at any grid size.
+__device__ void pivot0(const AssembleArgs& A) {
+  __shared__ double P[32 * SP], M[32 * SP], pv[32];
+  const int t = threadIdx.x;
+  if (t == 0) {
+    while (__hip_atomic_load(A.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ASM_SUB)
+      __builtin_amdgcn_s_sleep(1);
+    *A.flag = 0u;  // re-arm for the next step (no other user until then)
+  }
+  __syncthreads();
+  __threadfence();  // acquire: see the tile rows released by the assembling workgroups
+  for (int e = t; e < 1024; e += 256) P[(e >> 5) * SP + (e & 31)] = A.K[(size_t)(e >> 5) * A.p + (e & 31)];
+  __syncthreads();
+  const double k00 = P[0];
+  const double ls = pivot_chol_inv_block(P, M, pv, t, A.status);
+  for (int e = t; e < 1024; e += 256) A.piv[e] = M[(e >> 5) * SP + (e & 31)];
+  if (t == 0) {
+    A.ldet[0] = ls;
+    A.pst[0] = k00;   // refinement gate: K_00
+    A.pst[1] = 0.0;   // max diag K^{-1}, atomicMax'd by the last sweep
+  }
+}
+
 template <bool MATERN, bool COS, int DERIV>
 __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
   const int axis = blockIdx.y;
   const AssembleArgs& A = b.ax[axis];
+  const int t = threadIdx.x;
+  const bool pivot_wg = (int)blockIdx.x == b.pivot_x;
   const int tile = blockIdx.x / ASM_SUB, sub = blockIdx.x % ASM_SUB;
-  if (tile >= b.tiles[axis]) return;
+  if (!pivot_wg && tile >= b.tiles[axis]) return;
+
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
+  __shared__ double pk[4][64], pd[4][64];
+  if (t < q) axis_component(b.prep, axis, q, t, sw[t], sa[t], so[t]);
+  if (blockIdx.x == 0 && axis == 0) publish_prep(b.prep, q);
+  __syncthreads();
+  if (pivot_wg) {
+    pivot0(A);
+    return;
+  }
   int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
   while ((I + 1) * (I + 2) / 2 <= tile) ++I;
   while (I * (I + 1) / 2 > tile) --I;
   const int J = tile - I * (I + 1) / 2;
-
-  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
-  __shared__ double pk[4][64], pd[4][64];
-  const int t = threadIdx.x;
-  if (t < q) {
-    sw[t] = A.kc->w[t];
-    sa[t] = A.kc->a[t];
-    so[t] = A.kc->om[t];
-  }
-  __syncthreads();
   const int e = t & 63, g = t >> 6;
   const int i = I * 32 + 2 * sub + (e >> 5), j = J * 32 + (e & 31);
   const bool real = i < A.n && j < A.n;
@@ -114,6 +172,10 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
     if (A.Kc) A.Kc[(size_t)j * A.p + i] = kv;
     if (DERIV == 2) A.D[(size_t)j * A.p + i] = dv;
     if (DERIV == 1) A.D[(size_t)j * A.p + i] = real ? s_ji * dv : 0.0;
+  }
+  if (tile == 0 && b.pivot_x >= 0) {  // release this sub-block of tile (0,0) to pivot0
+    __threadfence();
+    if (t == 0) atomicAdd(A.flag, 1u);
   }
 }
 
@@ -187,7 +249,7 @@ hipError_t launch_pairs(int kind, int q, const double* x1, const double* x2, lon
 template <bool MATERN, bool COS>
 static void launch_assemble_t(const AssembleBatch& b, int naxes, int maxt, int q, int deriv,
                               hipStream_t s) {
-  dim3 grid(maxt * ASM_SUB, naxes);
+  dim3 grid(maxt * ASM_SUB + (b.pivot_x >= 0 ? 1 : 0), naxes);
   if (deriv == 2)
     hipLaunchKernelGGL((assemble_kernel<MATERN, COS, 2>), grid, dim3(256), 0, s, b, q);
   else if (deriv == 1)
@@ -196,7 +258,8 @@ static void launch_assemble_t(const AssembleBatch& b, int naxes, int maxt, int q
     hipLaunchKernelGGL((assemble_kernel<MATERN, COS, 0>), grid, dim3(256), 0, s, b, q);
 }
 
-hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, hipStream_t s) {
+hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, const PrepArgs& prep,
+                           hipStream_t s) {
   AssembleBatch b{};
   int maxt = 0;
   for (int k = 0; k < naxes; ++k) {
@@ -205,6 +268,10 @@ hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, hi
     b.tiles[k] = T * (T + 1) / 2;
     if (b.tiles[k] > maxt) maxt = b.tiles[k];
   }
+  b.prep = prep;
+  b.pivot_x = a[0].piv ? maxt * ASM_SUB : -1;
+  for (int k = 1; k < naxes; ++k)
+    if ((a[k].piv != nullptr) != (a[0].piv != nullptr)) return hipErrorInvalidValue;
   int deriv = a[0].deriv;
   switch (kind) {
     case SE_COS: launch_assemble_t<false, true>(b, naxes, maxt, q, deriv, s); break;

@@ -100,6 +100,7 @@ struct gpk_handle {
   std::vector<GemmDesc> hdescs;  // per-stage GEMM descriptors (kernel arguments)
   Stage st[kGemmStages];
   double *Kc[2] = {}, *pst[2] = {};  // kept K (refinement residuals), pivot stats (gate)
+  unsigned int* aflag[2] = {};        // assembly -> pivot-0 hand-off counters
   double* rvec = nullptr;            // 1D refinement residual
   // predict scratch
   GemmDesc* pdescs = nullptr;
@@ -141,9 +142,29 @@ static void mark(gpk_handle* h, int stage) {
 // ------------------------------------------------------------------------------------------
 // the step, in stream order
 // ------------------------------------------------------------------------------------------
-static int enqueue_assemble_inverse(gpk_handle* h) {
+static PrepArgs make_prep(gpk_handle* h, int apply) {
   const Layout& L = h->L;
-  AssembleArgs aa[2];
+  PrepArgs P{};
+  P.params = h->params;
+  P.off_kp[0] = L.off_kp[0];
+  P.off_kp[1] = L.off_kp[1];
+  P.off_tau = L.off_tau;
+  P.off_v = L.off_v;
+  P.naxes = L.naxes;
+  P.has_cos = (h->prob.kind == GPK_SE_COS || h->prob.kind == GPK_MATERN52_COS) ? 1 : 0;
+  P.kc = h->kc;
+  P.sc = h->sc;
+  P.count = h->count;
+  P.apply = apply;
+  P.b1 = h->hyper.b1;
+  P.b2 = h->hyper.b2;
+  return P;
+}
+
+// assemble K, D (+ step constants, + pivot block 0) and invert K: the first part of a step
+static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
+  const Layout& L = h->L;
+  AssembleArgs aa[2] = {};
   int deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
   for (int a = 0; a < L.naxes; ++a) {
     aa[a].x = a == 0 ? h->x1 : h->x2;
@@ -155,8 +176,13 @@ static int enqueue_assemble_inverse(gpk_handle* h) {
     aa[a].D = h->D[a];
     aa[a].deriv = deriv;
     aa[a].Kc = h->Kc[a];
+    aa[a].piv = h->piv[a];
+    aa[a].ldet = h->ldet[a];
+    aa[a].pst = h->pst[a];
+    aa[a].status = h->status;
+    aa[a].flag = h->aflag[a];
   }
-  TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, h->s), "assemble"));
+  TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, apply), h->s), "assemble"));
   mark(h, 1);
   SpdArgs sa[2];
   for (int a = 0; a < L.naxes; ++a) {
@@ -170,7 +196,7 @@ static int enqueue_assemble_inverse(gpk_handle* h) {
     sa[a].pst = h->pst[a];
   }
   double* fin[2] = {nullptr, nullptr};
-  TRY(check_launch(launch_spd_inverse(sa, L.naxes, fin, h->s), "spd_inverse"));
+  TRY(check_launch(launch_spd_inverse(sa, L.naxes, fin, h->s, true), "spd_inverse"));
   for (int a = 0; a < L.naxes; ++a) h->Kinv[a] = fin[a];
   mark(h, 2);
   return GPK_OK;
@@ -179,10 +205,8 @@ static int enqueue_assemble_inverse(gpk_handle* h) {
 static int enqueue_step(gpk_handle* h, int apply) {
   const Layout& L = h->L;
   if (h->profiling) (void)hipEventRecord(h->ev[0], h->s);
-  TRY(check_launch(launch_prep2(h->params, L, h->kc, h->sc, h->count, apply, h->hyper.b1,
-                                h->hyper.b2, h->s), "prep"));
-  mark(h, 0);
-  TRY(enqueue_assemble_inverse(h));
+  mark(h, 0);  // "prep" is fused into the assembly launch (stage kept for the name table)
+  TRY(enqueue_assemble_inverse(h, apply));
   int stage = 3;
   const int ac = h->prob.eq == GPK_ALLENCAHN;
   if (L.dim == 2) {
@@ -635,6 +659,7 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
     A_(h->ldet[a], P / 32);
     A_(h->Kc[a], (size_t)P * P);
     A_(h->pst[a], 2);
+    A_(h->aflag[a], 1);
     h->nldet[a] = P / 32;
   }
   if (L.dim == 2) {
@@ -801,10 +826,9 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
   if (L.dim == 2 && (!xte2 || m2 <= 0)) return fail(GPK_EINVAL, "2D predict needs xte2");
   DevSwitch ds(h->dev);
   // K^{-1} at the current params
-  TRY(check_launch(launch_prep2(h->params, L, h->kc, h->sc, h->count, 0, h->hyper.b1, h->hyper.b2, h->s), "prep"));
   bool prof = h->profiling;
   h->profiling = false;
-  int rc = enqueue_assemble_inverse(h);
+  int rc = enqueue_assemble_inverse(h, 0);
   h->profiling = prof;
   TRY(rc);
   const int M1p = pad_up(m1), P1 = L.p1;
@@ -928,21 +952,20 @@ int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us) {
   if (!h || !avg_us || iters <= 0) return fail(GPK_EINVAL, "bad argument");
   DevSwitch ds(h->dev);
   const Layout& L = h->L;
-  TRY(check_launch(launch_prep2(h->params, L, h->kc, h->sc, h->count, 0, h->hyper.b1, h->hyper.b2, h->s), "prep"));
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
   double total = 0.0;
   for (int it = 0; it < iters; ++it) {
     // re-assemble K (the inverse consumes it), time only the inverse
-    AssembleArgs aa[2];
+    AssembleArgs aa[2] = {};
     const int deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
     for (int a = 0; a < L.naxes; ++a) {
       aa[a].x = a == 0 ? h->x1 : h->x2; aa[a].n = a == 0 ? L.n1 : L.n2; aa[a].p = a == 0 ? L.p1 : L.p2;
       aa[a].kc = h->kc + a; aa[a].jitter = h->prob.jitter; aa[a].K = h->K[a]; aa[a].D = h->D[a];
       aa[a].deriv = deriv; aa[a].Kc = nullptr;
     }
-    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, h->s), "assemble"));
+    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
     SpdArgs sa[2];
     for (int a = 0; a < L.naxes; ++a) {
       sa[a].X = h->K[a]; sa[a].Y = h->Kb[a]; sa[a].p = a == 0 ? L.p1 : L.p2; sa[a].n = a == 0 ? L.n1 : L.n2;
@@ -1098,7 +1121,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
   TRY(gpk_loss_grad(h, &loss, nullptr));
   DevSwitch ds(h->dev);
   const int deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
-  AssembleArgs aa[2];
+  AssembleArgs aa[2] = {};
   SpdArgs sa[2];
   for (int a = 0; a < L.naxes; ++a) {
     aa[a].x = a == 0 ? h->x1 : h->x2; aa[a].n = a == 0 ? L.n1 : L.n2; aa[a].p = a == 0 ? L.p1 : L.p2;
@@ -1113,7 +1136,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
   const double n1 = L.n1, n2 = L.dim == 2 ? L.n2 : 0.0;
   if (nm == "sweep") {
     // re-assemble K and factor pivot 0, then time sweep 0 (idempotent: X -> Y, piv[1]).
-    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, h->s), "assemble"));
+    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
     TRY(check_launch(launch_spd_stage(sa, L.naxes, -1, h->s), "pivot_init"));
     launch = [&]() { return launch_spd_stage(sa, L.naxes, 0, h->s); };
     // potrf+potri-equivalent flops (n^3 per factor) spread over the T = p/32 sweeps;
@@ -1124,7 +1147,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
       bytes += 16.0 * n * n;
     }
   } else if (nm == "assemble") {
-    launch = [&]() { return launch_assemble(h->prob.kind, L.q, aa, L.naxes, h->s); };
+    launch = [&]() { return launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s); };
     // K and D written (8 B each per element); flops not counted (transcendental-bound)
     for (int a = 0; a < L.naxes; ++a) { const double n = a == 0 ? n1 : n2; bytes += 16.0 * n * n; }
   } else if (nm == "gemm_B" && L.dim == 2) {

@@ -81,6 +81,21 @@ __device__ __forceinline__ void radial_l(double d, double a, double& m0, double&
 // ------------------------------------------------------------------------------------------
 namespace gpk {
 
+// Per-step constants from the flat params (kernel constants per axis, tau, v, the Adam step
+// counter and bias corrections).  Computed inside the assembly kernel: every workgroup derives
+// its axis constants itself and workgroup (0, 0) publishes them for the later kernels.
+struct PrepArgs {
+  const double* params;
+  int off_kp[2];       // start of (freq, log-ls, log-w) per axis
+  int off_tau, off_v;
+  int naxes, has_cos;
+  AxisConst* kc;       // out [naxes]
+  StepScalars* sc;     // out
+  int* count;          // Adam step counter (incremented when apply)
+  int apply;
+  double b1, b2;
+};
+
 struct AssembleArgs {
   const double* x;       // coords [n] (padded buffer ok)
   int n;                 // true size
@@ -91,8 +106,13 @@ struct AssembleArgs {
   double* Kc;            // [p*p]  kept copy of K for iterative refinement (nullable)
   double* D;             // [p*p]
   int deriv;             // 1 or 2 (0: K only)
+  // pivot block 0 of the SPD inverse, factored by one extra workgroup of the assembly launch
+  // (nullable piv: not fused).  Same outputs as the sweep's pivot_init.
+  double* piv; double* ldet; double* pst; int* status;
+  unsigned int* flag;    // zero-initialised counter (re-armed by the pivot workgroup)
 };
-hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, hipStream_t s);
+hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, const PrepArgs& prep,
+                           hipStream_t s);
 hipError_t launch_pairs(int kind, int q, const double* x1, const double* x2, long n,
                         const AxisConst* kc, int deriv, double* out, hipStream_t s);
 hipError_t launch_cross(int kind, int q, const double* xr, int nr, const double* xc, int nc,
@@ -111,7 +131,9 @@ struct SpdArgs {
   int* status;     // nonzero => not positive definite
 };
 // Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.
-hipError_t launch_spd_inverse(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
+// pivot0_done: pivot block 0 was already factored (by the assembly launch).
+hipError_t launch_spd_inverse(SpdArgs* args, int nmat, double** final_out, hipStream_t s,
+                              bool pivot0_done = false);
 hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
 
 // Iterative-refinement gate: a refinement GEMM/GEMV stores its result only when the factor's

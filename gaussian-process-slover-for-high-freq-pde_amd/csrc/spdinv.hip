@@ -22,6 +22,7 @@
 // pivot tile factors it in its tail, so the next launch finds L^{-1} ready: N/32 launches,
 // batched over both Kronecker factors.
 #include "gpk_internal.h"
+#include "spd_pivot.h"
 
 namespace gpk {
 
@@ -29,76 +30,6 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int SA = 34;  // LDS row stride for A-role tiles (conflict-free ds_read_b64 A[i][k])
 constexpr int SB = 48;  // LDS row stride for B-role tiles (conflict-free B[k][j])
-constexpr int SP = 33;  // pivot scratch stride
-
-// One workgroup (256 threads): Cholesky of the 32x32 SPD block A = L L^T (LDS, stride SP,
-// full symmetric storage) and M = L^{-1} (LDS, stride SP).  Thread t owns column c = t&31,
-// rows i = (t>>5) + 8r (r = 0..3) of both.  Right-looking step k:
-//   p = A[k][k], rs = 1/sqrt(p);  l_ic = A[k][i] rs (row k = column k by symmetry)
-//   A[i][c] -= l_ik l_ck  (i, c > k)          M[i][c] -= l_ik (rs M[k][c])  (i > k)
-// Row k of M is scaled by rs lazily (after the loop), so step k writes only rows > k and one
-// barrier per step orders everything.  The serial chain per step is one LDS read, v_rsq_f64
-// + two Newton steps (no fp64 sqrt/div sequences), a few FMAs, the barrier; the log det
-// (sum_k log p_k) is formed after the loop, one log per lane.  Returns it in thread 0.
-__device__ __forceinline__ double rsqrt_f64(double p) {
-  double y = __builtin_amdgcn_rsq(p);          // ~2^-29 relative
-  double e = fma(-p * y, y, 1.0);              // 1 - p y^2
-  y = fma(0.5 * y, e, y);
-  e = fma(-p * y, y, 1.0);
-  return fma(0.5 * y, e, y);
-}
-
-__device__ __forceinline__ double pivot_chol_inv_block(double* A, double* M, double* pv, int t,
-                                                       int* status) {
-  const int c = t & 31, i0 = t >> 5;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) M[(i0 + 8 * r) * SP + c] = (i0 + 8 * r == c) ? 1.0 : 0.0;
-  __syncthreads();
-  for (int k = 0; k < 32; ++k) {
-    // all LDS reads of the step first (one wait), then branch-free math, then the writes;
-    // rows <= k are rewritten with their unchanged value (benign: same bits)
-    const double p = A[k * SP + k];
-    const double akc = A[k * SP + c], mkc0 = M[k * SP + c];
-    double aki[4], aic[4], mic[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + 8 * r;
-      aki[r] = A[k * SP + i];
-      aic[r] = A[i * SP + c];
-      mic[r] = M[i * SP + c];
-    }
-    const double rs = rsqrt_f64(p);
-    if (t == 0) pv[k] = p;
-    const double lck = akc * rs, mkc = mkc0 * rs;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + 8 * r;
-      const double lik = aki[r] * rs;
-      const double na = (i > k && c > k) ? fma(-lik, lck, aic[r]) : aic[r];
-      const double nm = (i > k) ? fma(-lik, mkc, mic[r]) : mic[r];
-      A[i * SP + c] = na;
-      M[i * SP + c] = nm;
-    }
-    __syncthreads();
-  }
-  // lazy row scaling of L^{-1}; log det from the 32 pivots
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = i0 + 8 * r;
-    M[i * SP + c] *= rsqrt_f64(pv[i]);
-  }
-  double ls = 0.0;
-  if (t < 64) {
-    const double pk = pv[t & 31];
-    if (t < 32 && !(pk > 0.0)) atomicOr(status, 1);
-    ls = (t < 32) ? log(pk) : 0.0;
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
-  }
-  __syncthreads();
-  return ls;
-}
-
 struct SpdBatch {
   double* X[2];   // buffer holding the assembled K (even sweeps read it)
   double* Y[2];   // pong buffer (odd sweeps read it)
@@ -259,7 +190,8 @@ hipError_t launch_spd_stage(SpdArgs* a, int nmat, int stage, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_spd_inverse(SpdArgs* a, int nmat, double** final_out, hipStream_t s) {
+hipError_t launch_spd_inverse(SpdArgs* a, int nmat, double** final_out, hipStream_t s,
+                              bool pivot0_done) {
   SpdBatch b{};
   int Tmax = 0;
   for (int m = 0; m < nmat; ++m) {
@@ -276,7 +208,7 @@ hipError_t launch_spd_inverse(SpdArgs* a, int nmat, double** final_out, hipStrea
     // sweep k reads (k even ? X : Y) and writes the other; T sweeps end in:
     final_out[m] = (b.T[m] & 1) ? a[m].Y : a[m].X;
   }
-  hipLaunchKernelGGL(pivot_init_kernel, dim3(nmat), dim3(256), 0, s, b);
+  if (!pivot0_done) hipLaunchKernelGGL(pivot_init_kernel, dim3(nmat), dim3(256), 0, s, b);
   for (int k = 0; k < Tmax; ++k)
     hipLaunchKernelGGL(sweep_kernel, dim3(Tmax * Tmax, nmat), dim3(256), 0, s, b, k);
   return hipGetLastError();
