@@ -90,11 +90,38 @@ __device__ void publish_prep(const PrepArgs& P, int q) {
     P.sc->bc1 = 1.0 - pow(P.b1, (double)n);
     P.sc->bc2 = 1.0 - pow(P.b2, (double)n);
   }
+  if (P.bgap) {
+    // u_b = hstack(U[0,:], U[-1,:], U[:,0], U[:,-1]) (2D) / u[Xind] (1D); fixed-order sum
+    double acc = 0.0;
+    if (P.dim == 2) {
+      const int n1 = P.n1, n2 = P.n2, nb = 2 * n2 + 2 * n1;
+      for (int k = t; k < nb; k += blockDim.x) {
+        int i, j;
+        if (k < n2) { i = 0; j = k; }
+        else if (k < 2 * n2) { i = n1 - 1; j = k - n2; }
+        else if (k < 2 * n2 + n1) { i = k - 2 * n2; j = 0; }
+        else { i = k - 2 * n2 - n1; j = n2 - 1; }
+        const double r = P.Up[(size_t)i * P.p2 + j] - P.bvals[k];
+        acc += r * r;
+      }
+    } else {
+      for (int k = t; k < P.nb; k += blockDim.x) {
+        const double r = P.Up[P.bidx[k]] - P.bvals[k];
+        acc += r * r;
+      }
+    }
+    __shared__ double sb[4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((t & 63) == 0) sb[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) *P.bgap = (sb[0] + sb[1]) + (sb[2] + sb[3]);
+  }
 }
 
 // Pivot block 0 (rows/cols 0..31) of the SPD inverse, factored inside the assembly launch by
 // one extra workgroup per axis.  The 16 workgroups that assemble tile (0,0) release their rows
-// (agent-scope fence, then a counter increment); the pivot workgroup waits for all 16, acquires,
+// (vmcnt drain, agent release, counter add); the pivot workgroup polls (sc1), acquires,
 // reads the tile and runs the Cholesky + L^{-1} of pivot_init.  It is dispatched after those
 // 16 (highest blockIdx.x), so they are resident or done: no deadlock at any grid size.
 __device__ void pivot0(const AssembleArgs& A) {
@@ -104,9 +131,10 @@ __device__ void pivot0(const AssembleArgs& A) {
     while (__hip_atomic_load(A.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ASM_SUB)
       __builtin_amdgcn_s_sleep(1);
     *A.flag = 0u;  // re-arm for the next step (no other user until then)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // see the released tile rows
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  __threadfence();  // acquire: see the tile rows released by the assembling workgroups
   for (int e = t; e < 1024; e += 256) P[(e >> 5) * SP + (e & 31)] = A.K[(size_t)(e >> 5) * A.p + (e & 31)];
   __syncthreads();
   const double k00 = P[0];
@@ -174,8 +202,12 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
     if (DERIV == 1) A.D[(size_t)j * A.p + i] = real ? s_ji * dv : 0.0;
   }
   if (tile == 0 && b.pivot_x >= 0) {  // release this sub-block of tile (0,0) to pivot0
-    __threadfence();
-    if (t == 0) atomicAdd(A.flag, 1u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (only wave 0 stored)
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      atomicAdd(A.flag, 1u);
+    }
   }
 }
 

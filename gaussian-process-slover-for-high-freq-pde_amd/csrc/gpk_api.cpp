@@ -42,12 +42,10 @@ namespace {
 constexpr int LOSS_CAP = 4096;
 const char* kStageNames1D[] = {"prep", "assemble", "spd_inverse", "gemv_alpha", "gemv_alpha_res",
                                "gemv_alpha_fix", "gemv_resid", "gemv_DtR", "gemv_beta",
-                               "gemv_beta_res", "gemv_beta_fix", "pgrad", "reduce", "finalize",
-                               "adam_u"};
+                               "gemv_beta_res", "gemv_beta_fix", "pgrad_tail"};
 const char* kStageNames2D[] = {"prep", "assemble", "spd_inverse", "gemm_A", "gemm_A_res",
                                "gemm_A_fix", "gemm_B", "gemm_B_res", "gemm_B_fix", "gemm_C",
-                               "gemm_D", "gemm_D_res", "gemm_D_fix", "gemm_E", "pgrad", "reduce",
-                               "finalize", "adam_u"};
+                               "gemm_D", "gemm_D_res", "gemm_D_fix", "gemm_E", "pgrad_tail"};
 constexpr int kMaxStages = 18;
 constexpr int kGemmStages = 11;  // A, A_res, A_fix, B, B_res, B_fix, C, D, D_res, D_fix, E
 
@@ -97,6 +95,10 @@ struct gpk_handle {
   int nquad = 0, negap = 0;
   double *pgpart = nullptr, *pg = nullptr;
   int bpa = 0;
+  // fused step tail (pgrad launch): group counters / partials, boundary gap
+  unsigned int *tcount = nullptr, *ttop = nullptr;
+  double *tgpart = nullptr, *bgap = nullptr;
+  int ttg = 0, tngpa = 0;
   std::vector<GemmDesc> hdescs;  // per-stage GEMM descriptors (kernel arguments)
   Stage st[kGemmStages];
   double *Kc[2] = {}, *pst[2] = {};  // kept K (refinement residuals), pivot stats (gate)
@@ -158,6 +160,9 @@ static PrepArgs make_prep(gpk_handle* h, int apply) {
   P.apply = apply;
   P.b1 = h->hyper.b1;
   P.b2 = h->hyper.b2;
+  P.Up = h->Up; P.bvals = h->bvals; P.bidx = h->bidx; P.nb = h->prob.nb;
+  P.dim = L.dim; P.n1 = L.n1; P.n2 = L.n2; P.p2 = L.p2;
+  P.bgap = h->bgap;
   return P;
 }
 
@@ -202,6 +207,33 @@ static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
   return GPK_OK;
 }
 
+// the step tail (loss, small-parameter Adam, dL/dU + Adam on U) fused into the pgrad launch
+static TailArgs make_tail(gpk_handle* h, int apply) {
+  const Layout& L = h->L;
+  const int ac = h->prob.eq == GPK_ALLENCAHN;
+  TailArgs T{};
+  T.fused = 1;
+  FinalizeArgs& f = T.fin;
+  f.L = L; f.hyper = h->hyper; f.llk_weight = h->prob.llk_weight; f.logdet = h->prob.logdet;
+  f.apply = apply; f.has_cos = kind_cos(h->prob.kind);
+  f.red_quad = h->red_quad; f.nquad = h->nquad; f.red_egap = h->red_egap; f.negap = h->negap;
+  for (int a = 0; a < L.naxes; ++a) { f.ldet[a] = h->ldet[a]; f.nldet[a] = h->nldet[a]; }
+  f.pg = h->pg; f.kc = h->kc; f.sc = h->sc; f.Up = h->Up; f.bvals = h->bvals;
+  f.bidx = h->bidx; f.nb = h->prob.nb;
+  f.params = h->params; f.grad = h->grad; f.m = h->m; f.v = h->v;
+  f.losses = h->losses; f.loss_slot = h->loss_slot; f.diag = h->diag;
+  f.bgap = h->bgap;
+  AdamUArgs& au = T.adam;
+  au.L = L; au.hyper = h->hyper; au.llk_weight = h->prob.llk_weight; au.apply = apply; au.ac = ac;
+  au.sc = h->sc; au.Up = h->Up; au.bvals = h->bvals; au.bidx = h->bidx; au.nb = h->prob.nb;
+  au.params = h->params; au.grad = h->grad; au.m = h->m; au.v = h->v;
+  if (L.dim == 2) { au.S = h->S; au.X1 = h->X1; au.X2 = h->X2; au.R = h->R; }
+  else { au.S = nullptr; au.X1 = h->alpha; au.X2 = h->beta; au.R = h->R; }
+  T.gcount = h->tcount; T.top = h->ttop; T.gpart = h->tgpart; T.pg = h->pg;
+  T.tg = h->ttg; T.ngpa = h->tngpa;
+  return T;
+}
+
 static int enqueue_step(gpk_handle* h, int apply) {
   const Layout& L = h->L;
   if (h->profiling) (void)hipEventRecord(h->ev[0], h->s);
@@ -227,7 +259,8 @@ static int enqueue_step(gpk_handle* h, int apply) {
       pa[a].deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
     }
-    TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s), "pgrad"));
+    TailArgs tail = make_tail(h, apply);
+    TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, &tail), "pgrad"));
     mark(h, stage++);
   } else {
     const int P = L.p1;
@@ -266,30 +299,10 @@ static int enqueue_step(gpk_handle* h, int apply) {
     pa.x = h->x1; pa.n = L.n1; pa.p = P; pa.kc = h->kc;
     pa.Kinv = h->Kinv[0]; pa.alpha = h->alpha; pa.beta = h->beta; pa.R = h->R;
     pa.halfc = 0.5 * h->prob.logdet; pa.deriv = 2; pa.part = h->pgpart;
-    TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 1, &pa, 1, h->bpa, h->sc, h->s), "pgrad"));
+    TailArgs tail = make_tail(h, apply);
+    TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 1, &pa, 1, h->bpa, h->sc, h->s, &tail), "pgrad"));
     mark(h, stage++);
   }
-  TRY(check_launch(launch_reduce_parts(h->pgpart, h->bpa, L.naxes, L.q, h->pg, h->s), "reduce"));
-  mark(h, stage++);
-  FinalizeArgs f{};
-  f.L = L; f.hyper = h->hyper; f.llk_weight = h->prob.llk_weight; f.logdet = h->prob.logdet;
-  f.apply = apply; f.has_cos = kind_cos(h->prob.kind);
-  f.red_quad = h->red_quad; f.nquad = h->nquad; f.red_egap = h->red_egap; f.negap = h->negap;
-  for (int a = 0; a < L.naxes; ++a) { f.ldet[a] = h->ldet[a]; f.nldet[a] = h->nldet[a]; }
-  f.pg = h->pg; f.kc = h->kc; f.sc = h->sc; f.Up = h->Up; f.bvals = h->bvals;
-  f.bidx = h->bidx; f.nb = h->prob.nb;
-  f.params = h->params; f.grad = h->grad; f.m = h->m; f.v = h->v;
-  f.losses = h->losses; f.loss_slot = h->loss_slot; f.diag = h->diag;
-  TRY(check_launch(launch_finalize(f, h->s), "finalize"));
-  mark(h, stage++);
-  AdamUArgs au{};
-  au.L = L; au.hyper = h->hyper; au.llk_weight = h->prob.llk_weight; au.apply = apply; au.ac = ac;
-  au.sc = h->sc; au.Up = h->Up; au.bvals = h->bvals; au.bidx = h->bidx; au.nb = h->prob.nb;
-  au.params = h->params; au.grad = h->grad; au.m = h->m; au.v = h->v;
-  if (L.dim == 2) { au.S = h->S; au.X1 = h->X1; au.X2 = h->X2; au.R = h->R; }
-  else { au.S = nullptr; au.X1 = h->alpha; au.X2 = h->beta; au.R = h->R; }
-  TRY(check_launch(launch_adam_u(au, h->s), "adam_u"));
-  mark(h, stage++);
   h->nstage = stage;
   return GPK_OK;
 }
@@ -681,6 +694,12 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
   h->bpa = std::max(pgrad_blocks(L.n1), L.dim == 2 ? pgrad_blocks(L.n2) : 0);
   A_(h->pgpart, (size_t)L.naxes * h->bpa * 3 * QMAX);
   A_(h->pg, (size_t)L.naxes * 3 * QMAX);
+  h->ttg = std::max(32, (int)std::ceil(std::sqrt((double)h->bpa)));
+  h->tngpa = (h->bpa + h->ttg - 1) / h->ttg;
+  A_(h->tcount, (size_t)L.naxes * h->tngpa);
+  A_(h->ttop, 1);
+  A_(h->tgpart, (size_t)L.naxes * h->tngpa * 3 * QMAX);
+  A_(h->bgap, 1);
 #undef A_
   // upload the problem
   if (hipMemcpyAsync(h->x1, p->x1, L.n1 * sizeof(double), hipMemcpyHostToDevice, h->s) != hipSuccess)

@@ -94,6 +94,11 @@ struct PrepArgs {
   int* count;          // Adam step counter (incremented when apply)
   int apply;
   double b1, b2;
+  // boundary gap ||u_b - b||^2 of U at the start of the step (model_GP_solver_2d.py:123-128,
+  // model_GP_solver_1d.py:101-106), taken here because the fused tail updates U in place
+  const double* Up; const double* bvals; const int* bidx;
+  int nb, dim, n1, n2, p2;
+  double* bgap;        // out [1]
 };
 
 struct AssembleArgs {
@@ -208,8 +213,11 @@ struct PGradArgs {
   int deriv;
   double* part;                           // [nblocks * 3*QMAX]
 };
+struct TailArgs;  // stepk.h
+// tail (nullable): the fused step tail carried by the same launch (stepk.h TailArgs)
 hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int naxes,
-                        int blocks_per_axis, const StepScalars* sc, hipStream_t s);
+                        int blocks_per_axis, const StepScalars* sc, hipStream_t s,
+                        const TailArgs* tail = nullptr);
 int pgrad_blocks(int n);
 
 }  // namespace gpk

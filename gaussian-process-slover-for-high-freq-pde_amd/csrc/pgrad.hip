@@ -16,6 +16,7 @@
 // the vectors alpha = K^{-1}u, beta = K^{-1}D^T R, R (model_GP_solver_1d.py:80-149):
 //   G_K = c/2 K^{-1} - 1/2 alpha alpha^T - v beta alpha^T,   G_D = v R alpha^T.
 #include "gpk_internal.h"
+#include "stepk_dev.h"
 
 namespace gpk {
 
@@ -25,16 +26,96 @@ constexpr int PG_SUB = 1024 / PAIRS;  // workgroups per tile
 struct PGradBatch {
   PGradArgs ax[2];
   int tiles[2];
+  int naxes, bpa;
+  TailArgs tail;
 };
+
+// Fused tail, run by every block of the gradient planes after its partial is stored: the last
+// block of each group of `tg` blocks sums the group's partials (block order), the last group
+// sums the group partials (group order) into pg and runs finalize_body.  Cross-XCD hand-off per
+// MI355X_MICROARCH.md §inter-workgroup visibility: producers store write-through (sc1), every
+// storing wave drains (vmcnt 0), a barrier, then ONE lane's agent-scope ticket add; the block
+// whose add came last does one agent acquire (+ vmcnt 0 + barrier) before reading.  No
+// __threadfence() per block (its L2 write-back made this tail 4x slower).  Counters are
+// re-armed by the blocks that consume them.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store sc1
+}
+
+__device__ __forceinline__ bool arrive_last(unsigned int* counter, unsigned int n, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(counter, 1u);
+    const bool last = prev == n - 1u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// sum_{k<n} p[k*stride] in index order, 16 loads in flight per batch (latency-bound chain)
+__device__ __forceinline__ double strided_sum(const double* p, int stride, int n) {
+  double acc = 0.0;
+  int k = 0;
+  for (; k + 16 <= n; k += 16) {
+    double v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = p[(size_t)(k + j) * stride];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc += v[j];
+  }
+  for (; k < n; ++k) acc += p[(size_t)k * stride];
+  return acc;
+}
+
+__device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
+  const TailArgs& T = b.tail;
+  __shared__ int s_last;
+  const int t = threadIdx.x;
+  const int gi = blk / T.tg;
+  const int gsize = min(T.tg, b.bpa - gi * T.tg);
+  if (!arrive_last(T.gcount + axis * T.ngpa + gi, (unsigned)gsize, &s_last)) return;
+  const double* part = b.ax[axis].part;
+  for (int x = t; x < 3 * QMAX; x += 256) {
+    double acc = 0.0;
+    if ((x % QMAX) < q)
+      acc = strided_sum(part + (size_t)gi * T.tg * (3 * QMAX) + x, 3 * QMAX, gsize);
+    st_wt(T.gpart + (size_t)(axis * T.ngpa + gi) * (3 * QMAX) + x, acc);
+  }
+  if (t == 0) T.gcount[axis * T.ngpa + gi] = 0u;  // re-arm (no other user this step)
+  if (!arrive_last(T.top, (unsigned)(b.naxes * T.ngpa), &s_last)) return;
+  for (int e = t; e < b.naxes * 3 * QMAX; e += 256) {
+    const int ax = e / (3 * QMAX), x = e % (3 * QMAX);
+    double acc = 0.0;
+    if ((x % QMAX) < q) acc = strided_sum(T.gpart + (size_t)ax * T.ngpa * (3 * QMAX) + x, 3 * QMAX, T.ngpa);
+    T.pg[e] = acc;
+  }
+  __syncthreads();  // pg (global) written by this block is visible to it after the barrier
+  if (t == 0) *T.top = 0u;
+  finalize_body(T.fin);
+}
 
 template <bool MATERN, bool COS, int DERIV, bool MODE1D>
 __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
                                                     const StepScalars* __restrict__ sc) {
   const int axis = blockIdx.y;
-  const PGradArgs& A = b.ax[axis];
   const int blk = blockIdx.x;
+  if (axis == b.naxes) {  // fused tail: dL/dU + Adam on U (grid-stride over the solution grid)
+    const int nu = tail_nu(b.tail.adam.L);
+    for (int e = blk * 256 + threadIdx.x; e < nu; e += gridDim.x * 256) adam_u_elem(b.tail.adam, e);
+    return;
+  }
+  const PGradArgs& A = b.ax[axis];
   const int tile = blk / PG_SUB, chunk = blk % PG_SUB;
-  if (tile >= b.tiles[axis]) return;
+  if (tile >= b.tiles[axis]) {  // no pairs here (shorter axis); its partial slot stays zero
+    if (b.tail.fused) pgrad_tail(b, axis, blk, q);
+    return;
+  }
   int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
   while ((I + 1) * (I + 2) / 2 <= tile) ++I;
   while (I * (I + 1) / 2 > tile) --I;
@@ -139,10 +220,14 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
       double s = 0.0;
 #pragma unroll
       for (int gg = 0; gg < 8; ++gg) s += sacc[gg][which][qq];
-      if (q0 + qq < QMAX) out[which * QMAX + q0 + qq] = s;
+      if (q0 + qq < QMAX) {
+        if (b.tail.fused) st_wt(out + which * QMAX + q0 + qq, s);  // write-through: handed off
+        else out[which * QMAX + q0 + qq] = s;
+      }
     }
     __syncthreads();
   }
+  if (b.tail.fused) pgrad_tail(b, axis, blk, q);
 }
 
 int pgrad_blocks(int n) {
@@ -153,7 +238,7 @@ int pgrad_blocks(int n) {
 template <bool MATERN, bool COS>
 static void launch_pg_t(const PGradBatch& b, int naxes, int bpa, int q, int deriv, int mode1d,
                         const StepScalars* sc, hipStream_t s) {
-  dim3 grid(bpa, naxes);
+  dim3 grid(bpa, naxes + (b.tail.fused ? 1 : 0));
   if (mode1d) {
     hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, true>), grid, dim3(256), 0, s, b, q, sc);
   } else if (deriv == 2) {
@@ -164,12 +249,20 @@ static void launch_pg_t(const PGradBatch& b, int naxes, int bpa, int q, int deri
 }
 
 hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int naxes,
-                        int blocks_per_axis, const StepScalars* sc, hipStream_t s) {
+                        int blocks_per_axis, const StepScalars* sc, hipStream_t s,
+                        const TailArgs* tail) {
   PGradBatch b{};
   for (int k = 0; k < naxes; ++k) {
     b.ax[k] = a[k];
     int T = a[k].p / 32;
     b.tiles[k] = T * (T + 1) / 2;
+  }
+  b.naxes = naxes;
+  b.bpa = blocks_per_axis;
+  if (tail) b.tail = *tail;
+  if (b.tail.fused) {
+    // every block of the gradient planes must exist: group sizes are sized on bpa
+    if (b.tail.tg <= 0 || b.tail.ngpa * b.tail.tg < blocks_per_axis) return hipErrorInvalidValue;
   }
   int deriv = a[0].deriv;
   switch (kind) {

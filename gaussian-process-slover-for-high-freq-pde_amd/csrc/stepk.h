@@ -36,6 +36,7 @@ struct FinalizeArgs {
   double* params; double* grad; double* m; double* v;
   double* losses; int* loss_slot;
   double* diag;              // [8]: loss, logdet1, logdet2, quad, egap, bgap
+  const double* bgap;        // [1] ||u_b - b||^2 at the start of the step (assembly launch)
 };
 
 struct AdamUArgs {
@@ -50,6 +51,21 @@ struct AdamUArgs {
   const double* bvals;
   const int* bidx; int nb;
   double* params; double* grad; double* m; double* v;
+};
+
+// Fused tail of a step, carried by the parameter-gradient launch (pgrad.hip): one extra grid
+// plane of blocks runs dL/dU + Adam on U, and the parameter-gradient partials are reduced by a
+// two-level "last block" scheme (fixed summation order: deterministic) whose final block runs
+// the loss / small-parameter Adam (finalize_body).
+struct TailArgs {
+  int fused;                 // 0: pgrad only (separate reduce/finalize/adam launches)
+  FinalizeArgs fin;
+  AdamUArgs adam;
+  unsigned int* gcount;      // [naxes * ngpa] level-1 counters (zero; re-armed in the kernel)
+  unsigned int* top;         // level-2 counter
+  double* gpart;             // [naxes * ngpa][3*QMAX] group partials
+  double* pg;                // [naxes][3*QMAX] reduced parameter gradients (-> fin.pg)
+  int tg, ngpa;              // blocks per group, groups per axis
 };
 
 hipError_t launch_prep2(const double* params, const Layout& L, AxisConst* kc, StepScalars* sc,
