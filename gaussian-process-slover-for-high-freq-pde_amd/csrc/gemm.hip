@@ -196,8 +196,8 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
   const int tn = d.N >> 4;
   const int tiles = (d.M >> 4) * tn;
   if ((int)blockIdx.x >= tiles) return;
-  // the refinement gate is only consulted before the stores, so its load overlaps the operand
-  // loads instead of adding a dependent round trip (a closed gate wastes a few us of MFMA)
+  // refinement gate: its (scalar) load is issued first and overlaps the epilogue prefetch; a
+  // closed gate ends the workgroup before any operand load (launch + one round trip)
   const bool open = gate_open(d.gate);
   const int i0 = (blockIdx.x / tn) * 16, j0 = (blockIdx.x % tn) * 16;
   __shared__ double part[2][4][256];
@@ -214,6 +214,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
 #pragma unroll
     for (int r = 0; r < 4; ++r) ein[r] = epi_fetch(d, i0 + (lane >> 4) + 4 * r, j0 + (lane & 15));
   }
+  if (!open) return;  // uniform
   int b0, b1;
   range(d.K, b0, b1);
   d4 acc1 = {0.0, 0.0, 0.0, 0.0}, acc2 = {0.0, 0.0, 0.0, 0.0};
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
     part[1][wv][lane * 4 + r] = acc2[r];
   }
   __syncthreads();
-  if (wv != 0 || !open) return;
+  if (wv != 0) return;
   double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
   if (d.vscale2) alpha2 *= sc->v;
