@@ -11,6 +11,8 @@
 // (A[i=l&15][k=l>>4], B[k=l>>4][j=l&15], C/D row=(l>>4)+4r, col=l&15).
 #include "gpk_internal.h"
 
+#include <algorithm>
+
 namespace gpk {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -264,6 +266,200 @@ hipError_t launch_gemm_batch(const GemmDesc* descs, int ndesc, int max_tiles,
     hipLaunchKernelGGL(gemm_small_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, b, sc);
   else
     hipLaunchKernelGGL(gemm_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, b, sc);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Throughput variant for large factors (N >= ~1500, e.g. the 4096^2 advection grid): a 64x64
+// output tile per 256-thread workgroup, each wave a 32x32 quadrant (2x2 v_mfma_f64_16x16x4
+// blocks, every A/B fragment used twice); K-steps of 32 through double-buffered LDS with one
+// barrier per step; the next K-step's operands are fetched global->registers (16-B loads,
+// coalesced along the contiguous dimension of each operand) while the current one is
+// multiplied.  Tiles are dealt XCD-major (blocks b, b+8, ... share an XCD and get consecutive
+// tiles, so they share A row panels in that XCD's L2).  Edge tiles of a 32-padded matrix are
+// half-empty: rows/cols >= M/N are skipped at load (zero) and store.
+// ---------------------------------------------------------------------------------------
+constexpr int BSA = 34;  // A-role LDS stride: [m][k], ds_read_b64 conflict-free (rows 4 banks apart)
+constexpr int BSB = 80;  // B-role LDS stride: [k][n], k and k+1 rows 32 banks apart
+
+struct BigRegs {
+  double2 a[4], b[4];
+};
+
+__device__ __forceinline__ void big_fetch(BigRegs& R, const double* A, int lda, int ta, const double* B,
+                                          int ldb, int tb, int M, int N, int i0, int j0, int k0,
+                                          int t) {
+  const double2 z = {0.0, 0.0};
+  if (!ta) {  // op(A)[i][k] = A[i][k]: row r = t>>2, k-chunk 8*(t&3)
+    const int r = t >> 2, kc = (t & 3) * 8;
+    const bool ok = i0 + r < M;
+    const double* p = A + (size_t)(i0 + r) * lda + k0 + kc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R.a[j] = ok ? *reinterpret_cast<const double2*>(p + 2 * j) : z;
+  } else {    // op(A)[i][k] = A[k][i]: k-row t>>3, i-chunk 8*(t&7)
+    const int kr = t >> 3, ic = (t & 7) * 8;
+    const double* p = A + (size_t)(k0 + kr) * lda + i0 + ic;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R.a[j] = (i0 + ic + 2 * j < M) ? *reinterpret_cast<const double2*>(p + 2 * j) : z;
+  }
+  if (!tb) {  // op(B)[k][j] = B[k][j]: k-row t>>3, j-chunk 8*(t&7)
+    const int kr = t >> 3, jc = (t & 7) * 8;
+    const double* p = B + (size_t)(k0 + kr) * ldb + j0 + jc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R.b[j] = (j0 + jc + 2 * j < N) ? *reinterpret_cast<const double2*>(p + 2 * j) : z;
+  } else {    // op(B)[k][j] = B[j][k]: j-row t>>2, k-chunk 8*(t&3)
+    const int r = t >> 2, kc = (t & 3) * 8;
+    const bool ok = j0 + r < N;
+    const double* p = B + (size_t)(j0 + r) * ldb + k0 + kc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R.b[j] = ok ? *reinterpret_cast<const double2*>(p + 2 * j) : z;
+  }
+}
+
+__device__ __forceinline__ void big_store(const BigRegs& R, double* sA, double* sB, int ta, int tb, int t) {
+  if (!ta) {
+    const int r = t >> 2, kc = (t & 3) * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<double2*>(sA + r * BSA + kc + 2 * j) = R.a[j];
+  } else {
+    const int kr = t >> 3, ic = (t & 7) * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sA[(ic + 2 * j) * BSA + kr] = R.a[j].x;
+      sA[(ic + 2 * j + 1) * BSA + kr] = R.a[j].y;
+    }
+  }
+  if (!tb) {
+    const int kr = t >> 3, jc = (t & 7) * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<double2*>(sB + kr * BSB + jc + 2 * j) = R.b[j];
+  } else {
+    const int r = t >> 2, kc = (t & 3) * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sB[(kc + 2 * j) * BSB + r] = R.b[j].x;
+      sB[(kc + 2 * j + 1) * BSB + r] = R.b[j].y;
+    }
+  }
+}
+
+// acc[bi][bj] += the wave's 32x32 quadrant (wr, wc) of one 32-deep K-step
+__device__ __forceinline__ void big_mma(const double* sA, const double* sB, int wr, int wc, int lane,
+                                        d4 (&acc)[2][2]) {
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const int k = 4 * kk + lk;
+    const double a0 = sA[(32 * wr + li) * BSA + k], a1 = sA[(32 * wr + 16 + li) * BSA + k];
+    const double b0 = sB[k * BSB + 32 * wc + li], b1 = sB[k * BSB + 32 * wc + 16 + li];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void big_product(const double* A, int lda, int ta, const double* B, int ldb,
+                                            int tb, int K, int M, int N, int i0, int j0, double* sA0,
+                                            double* sB0, int t, int wr, int wc, int lane,
+                                            d4 (&acc)[2][2]) {
+  constexpr int SAZ = 64 * BSA, SBZ = 32 * BSB;
+  BigRegs R;
+  const int nk = K >> 5;
+  big_fetch(R, A, lda, ta, B, ldb, tb, M, N, i0, j0, 0, t);
+  big_store(R, sA0, sB0, ta, tb, t);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) big_fetch(R, A, lda, ta, B, ldb, tb, M, N, i0, j0, (kt + 1) * 32, t);
+    big_mma(sA0 + cur * SAZ, sB0 + cur * SBZ, wr, wc, lane, acc);
+    if (kt + 1 < nk) big_store(R, sA0 + (cur ^ 1) * SAZ, sB0 + (cur ^ 1) * SBZ, ta, tb, t);
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void gemm_big_kernel(GemmBatch batch, const StepScalars* __restrict__ sc,
+                                                       int per_xcd) {
+  const GemmDesc& d = batch.d[blockIdx.y];
+  const int tn = (d.N + 63) >> 6;
+  const int tiles = ((d.M + 63) >> 6) * tn;
+  const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);  // XCD-major dealing
+  if (tile >= tiles) return;
+  if (!gate_open(d.gate)) return;  // refinement not needed (uniform)
+  const int i0 = (tile / tn) * 64, j0 = (tile % tn) * 64;
+  __shared__ double sA[2 * 64 * BSA], sB[2 * 32 * BSB];
+  __shared__ double sred[4], sred2[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  d4 acc1[2][2], acc2[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      acc1[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+      acc2[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+  big_product(d.A, d.lda, d.ta, d.B, d.ldb, d.tb, d.K, d.M, d.N, i0, j0, sA, sB, t, wr, wc, lane, acc1);
+  if (d.K2) big_product(d.A2, d.lda2, d.ta2, d.B2, d.ldb2, d.tb2, d.K2, d.M, d.N, i0, j0, sA, sB, t, wr, wc, lane, acc2);
+  double alpha = d.alpha, alpha2 = d.alpha2;
+  if (d.vscale) alpha *= sc->v;
+  if (d.vscale2) alpha2 *= sc->v;
+  double part = 0.0, part2 = 0.0;
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i0 + 32 * wr + 16 * bi + (lane >> 4) + 4 * r;
+        const int col = j0 + 32 * wc + 16 * bj + (lane & 15);
+        if (row < d.M && col < d.N) {
+          const EpiIn e = epi_fetch(d, row, col);
+          double c = alpha * acc1[bi][bj][r];
+          if (d.K2) c += alpha2 * acc2[bi][bj][r];
+          d.C[(size_t)row * d.ldc + col] = epi_apply(d, c, e, part, part2);
+        }
+      }
+  if (d.red) {
+    double s = block_sum_256(part, sred);
+    if (t == 0) d.red[tile] = s;
+  }
+  if (d.red2) {
+    double s = block_sum_256(part2, sred2);
+    if (t == 0) d.red2[tile] = s;
+  }
+}
+
+int gemm_tiles(const GemmDesc& d, int variant) {
+  if (variant == GEMM_SMALL) return (d.M / 16) * (d.N / 16);
+  if (variant == GEMM_BIG) return ((d.M + 63) / 64) * ((d.N + 63) / 64);
+  return (d.M / 32) * (d.N / 32);
+}
+
+int gemm_variant(const GemmDesc* descs, int ndesc, int force_big) {
+  if (force_big) return GEMM_BIG;
+  long tot16 = 0;
+  for (int i = 0; i < ndesc; ++i) tot16 += (long)(descs[i].M / 16) * (descs[i].N / 16);
+  return gemm_use_small(tot16) ? GEMM_SMALL : GEMM_BIG;
+}
+
+hipError_t launch_gemm_auto(const GemmDesc* descs, int ndesc, const StepScalars* sc, hipStream_t s,
+                            int variant) {
+  if (ndesc < 1 || ndesc > GEMM_MAX_BATCH) return hipErrorInvalidValue;
+  GemmBatch b{};
+  int mt = 0;
+  for (int i = 0; i < ndesc; ++i) {
+    b.d[i] = descs[i];
+    mt = std::max(mt, gemm_tiles(descs[i], variant));
+  }
+  if (variant == GEMM_SMALL) {
+    hipLaunchKernelGGL(gemm_small_kernel, dim3(mt, ndesc), dim3(256), 0, s, b, sc);
+  } else if (variant == GEMM_BIG) {
+    const int per = (mt + 7) / 8;
+    hipLaunchKernelGGL(gemm_big_kernel, dim3(8 * per, ndesc), dim3(256), 0, s, b, sc, per);
+  } else {
+    hipLaunchKernelGGL(gemm_kernel, dim3(mt, ndesc), dim3(256), 0, s, b, sc);
+  }
   return hipGetLastError();
 }
 

@@ -61,7 +61,7 @@ struct DevSwitch {  // restore the caller's current device on scope exit
 };
 
 struct Stage {
-  int off = 0, n = 0, maxtiles = 0, small = 0;
+  int off = 0, n = 0, variant = 0;
 };
 
 }  // namespace
@@ -243,8 +243,8 @@ static int enqueue_step(gpk_handle* h, int apply) {
   const int ac = h->prob.eq == GPK_ALLENCAHN;
   if (L.dim == 2) {
     for (int k = 0; k < kGemmStages; ++k) {
-      TRY(check_launch(launch_gemm_batch(h->hdescs.data() + h->st[k].off, h->st[k].n, h->st[k].maxtiles,
-                                         h->sc, h->s, h->st[k].small), "gemm"));
+      TRY(check_launch(launch_gemm_auto(h->hdescs.data() + h->st[k].off, h->st[k].n, h->sc, h->s,
+                                        h->st[k].variant), "gemm"));
       mark(h, stage++);
     }
     PGradArgs pa[2];
@@ -321,17 +321,10 @@ static int build_descs(gpk_handle* h) {
     return g;
   };
   auto begin = [&](int k) { h->st[k].off = (int)d.size(); };
+  const int force_big = (h->prob.flags & GPK_FLAG_FORCE_BIG_GEMM) ? 1 : 0;
   auto end = [&](int k) {
     h->st[k].n = (int)d.size() - h->st[k].off;
-    int mt32 = 0, mt16 = 0;
-    long tot16 = 0;
-    for (int i = h->st[k].off; i < (int)d.size(); ++i) {
-      mt32 = std::max(mt32, (d[i].M / 32) * (d[i].N / 32));
-      mt16 = std::max(mt16, (d[i].M / 16) * (d[i].N / 16));
-      tot16 += (long)(d[i].M / 16) * (d[i].N / 16);
-    }
-    h->st[k].small = gemm_use_small(tot16) ? 1 : 0;
-    h->st[k].maxtiles = h->st[k].small ? mt16 : mt32;
+    h->st[k].variant = gemm_variant(d.data() + h->st[k].off, h->st[k].n, force_big);
   };
   // Every solve against K (JAX: LU solves, model_GP_solver_2d.py:104-105 and the reverse
   // pass) is X = K^{-1} B (MFMA) plus one refinement X += K^{-1}(B - K X), whose two GEMMs are
@@ -451,7 +444,12 @@ static int build_descs(gpk_handle* h) {
     d.push_back(g2);
   }
   end(10);
-  h->nquad = h->negap = h->st[3].small ? (P1 / 16) * (P2 / 16) : (P1 / 32) * (P2 / 32);
+  {  // the residual descriptor of stage B carries the egap / quad partials: one per tile
+    int nq = 0;
+    for (int i = h->st[3].off; i < h->st[3].off + h->st[3].n; ++i)
+      if (d[i].red) nq = gemm_tiles(d[i], h->st[3].variant);
+    h->nquad = h->negap = nq;
+  }
   for (int k = 0; k < kGemmStages; ++k)
     if (h->st[k].n > GEMM_MAX_BATCH) return fail(GPK_EINVAL, "internal: GEMM stage batch too large");
   h->hdescs = d;
@@ -915,11 +913,9 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
     d[5].beta = 1.0; d[5].C0 = Sw; d[5].ldc0 = P2;
     mk(d[6], Kmn1, P1, 0, Sw, P2, 0, Mw, P2, M1p, P2, P1);
     mk(d[7], Mw, P2, 0, Kmn2, P2, 1, res, M2p, M1p, M2p, P2);
-    for (int k = 0; k < 8; ++k) {
-      const long t16 = (long)(d[k].M / 16) * (d[k].N / 16);
-      const int small = gemm_use_small(t16) ? 1 : 0;
-      (void)launch_gemm_batch(d + k, 1, small ? (int)t16 : (d[k].M / 32) * (d[k].N / 32), h->sc, h->s, small);
-    }
+    const int force_big = (h->prob.flags & GPK_FLAG_FORCE_BIG_GEMM) ? 1 : 0;
+    for (int k = 0; k < 8; ++k)
+      (void)launch_gemm_auto(d + k, 1, h->sc, h->s, gemm_variant(d + k, 1, force_big));
     for (int i = 0; i < m1; ++i)
       (void)hipMemcpyAsync(out + (size_t)i * m2, res + (size_t)i * M2p, m2 * sizeof(double),
                            hipMemcpyDeviceToHost, h->s);
@@ -1107,9 +1103,8 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
       g.A = h->Bt; g.lda = P2; g.B = h->D[1]; g.ldb = P2; g.tb = 1; g.K = P2;
     }
     g.C = tmp; g.ldc = P2; g.M = P1; g.N = P2; g.alpha = 1.0; g.epi = EPI_STORE;
-    const long t16 = (long)(P1 / 16) * (P2 / 16);
-    const int small = gemm_use_small(t16) ? 1 : 0;
-    hipError_t e = launch_gemm_batch(&g, 1, small ? (int)t16 : (P1 / 32) * (P2 / 32), h->sc, h->s, small);
+    hipError_t e = launch_gemm_auto(&g, 1, h->sc, h->s,
+                                    gemm_variant(&g, 1, (h->prob.flags & GPK_FLAG_FORCE_BIG_GEMM) ? 1 : 0));
     if (e != hipSuccess) { cleanup(); return fail(GPK_EHIP, hipGetErrorString(e)); }
     src = tmp;
   }
@@ -1171,8 +1166,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     for (int a = 0; a < L.naxes; ++a) { const double n = a == 0 ? n1 : n2; bytes += 16.0 * n * n; }
   } else if (nm == "gemm_B" && L.dim == 2) {
     launch = [&]() {
-      return launch_gemm_batch(h->hdescs.data() + h->st[3].off, h->st[3].n, h->st[3].maxtiles, h->sc, h->s,
-                               h->st[3].small);
+      return launch_gemm_auto(h->hdescs.data() + h->st[3].off, h->st[3].n, h->sc, h->s, h->st[3].variant);
     };
     // S = A K2^{-1} (2 n1 n2^2); R = D1 A + Bt D2^T (2 n1^2 n2 + 2 n1 n2^2)
     flops = 2 * n1 * n2 * n2 + 2 * n1 * n1 * n2 + 2 * n1 * n2 * n2;

@@ -181,6 +181,13 @@ hipError_t launch_gemm_batch(const GemmDesc* descs, int ndesc, int max_tiles,
                              const StepScalars* sc, hipStream_t s, int small);
 // heuristic: use the 16x16 latency kernel while the whole stage has few enough tiles
 inline bool gemm_use_small(long tiles16_total) { return tiles16_total <= 16384; }
+enum { GEMM_TILED32 = 0, GEMM_SMALL = 1, GEMM_BIG = 2 };
+// variant for a batch (force_big: the 64x64 throughput kernel regardless of size), tiles of a
+// descriptor under a variant (= the entries its red/red2 partials fill), and the launcher
+int gemm_variant(const GemmDesc* descs, int ndesc, int force_big);
+int gemm_tiles(const GemmDesc& d, int variant);
+hipError_t launch_gemm_auto(const GemmDesc* descs, int ndesc, const StepScalars* sc, hipStream_t s,
+                            int variant);
 
 __device__ __forceinline__ bool gate_open(const double* gate) {
   if (!gate) return true;

@@ -18,9 +18,13 @@
 #include "gpk_internal.h"
 #include "stepk_dev.h"
 
+#ifndef GPK_PG_PAIRS
+#define GPK_PG_PAIRS 64
+#endif
+
 namespace gpk {
 
-constexpr int PAIRS = 64;   // pairs per workgroup = 2 rows x 32 cols of a 32x32 tile
+constexpr int PAIRS = GPK_PG_PAIRS;  // pairs per workgroup (PAIRS/32 rows x 32 cols of a 32x32 tile)
 constexpr int PG_SUB = 1024 / PAIRS;  // workgroups per tile
 
 struct PGradBatch {

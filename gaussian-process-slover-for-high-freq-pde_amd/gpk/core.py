@@ -51,7 +51,7 @@ def params_template(dim, n1, n2, Q):
 class DeviceSolver:
     def __init__(self, dim, eq, kind, x1, src, bvals, x2=None, bidx=None, Q=30, jitter=1e-6,
                  llk_weight=200.0, logdet=True, beta=1.0, lr=0.01, freq_scale=20.0, device=0,
-                 b1=0.9, b2=0.999, eps=1e-8):
+                 b1=0.9, b2=0.999, eps=1e-8, flags=0):
         lib = _lib.load()
         self.dim = int(dim)
         self.eq = eq
@@ -84,6 +84,7 @@ class DeviceSolver:
         p.jitter, p.llk_weight, p.logdet, p.beta = jitter, llk_weight, float(logdet), beta
         p.lr, p.b1, p.b2, p.eps = lr, b1, b2, eps
         p.device = device
+        p.flags = int(flags)
         self._prob = p
         h = ctypes.c_void_p()
         check(lib.gpk_create(ctypes.byref(p), float(freq_scale), ctypes.byref(h)))

@@ -70,8 +70,11 @@ typedef struct gpk_problem {
   double beta;          /* advection speed (advection-sin.yaml:16); ignored otherwise */
   double lr, b1, b2, eps; /* optax.adam(lr) defaults b1=.9, b2=.999, eps=1e-8 */
   int32_t device;       /* HIP device ordinal */
-  int32_t flags;        /* reserved, 0 */
+  int32_t flags;        /* GPK_FLAG_* bits, normally 0 */
 } gpk_problem;
+
+/* gpk_problem.flags bits */
+#define GPK_FLAG_FORCE_BIG_GEMM 1 /* use the 64x64 throughput GEMM at every size (tests/tuning) */
 
 typedef struct gpk_handle gpk_handle;
 

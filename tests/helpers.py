@@ -35,16 +35,17 @@ def problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=24, n2=20, Q=5, seed=0, 
     return prob, params, (Xte, ute), fs
 
 
-def device_solver(prob, Q, fs=20.0, lr=0.01):
+def device_solver(prob, Q, fs=20.0, lr=0.01, flags=0):
     from gpk.core import DeviceSolver
     if "x" in prob:
         return DeviceSolver(1, prob["eq"], prob["kind"], prob["x"], prob["src"], prob["y"],
                             bidx=prob["xind"], Q=Q, jitter=prob["jitter"],
                             llk_weight=prob["llk_weight"], logdet=prob["logdet"], lr=lr,
-                            freq_scale=fs)
+                            freq_scale=fs, flags=flags)
     return DeviceSolver(2, prob["eq"], prob["kind"], prob["x1"], prob["src"], prob["bvals"],
                         x2=prob["x2"], Q=Q, jitter=prob["jitter"], llk_weight=prob["llk_weight"],
-                        logdet=prob["logdet"], beta=prob.get("beta", 1.0), lr=lr, freq_scale=fs)
+                        logdet=prob["logdet"], beta=prob.get("beta", 1.0), lr=lr, freq_scale=fs,
+                        flags=flags)
 
 
 def rel(a, b):

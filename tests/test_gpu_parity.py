@@ -78,12 +78,12 @@ def oracle_err(prob, params):
     return lo, go, errs
 
 
-def _cmp_lossgrad(prob, params, Q, fs, tol=None):
+def _cmp_lossgrad(prob, params, Q, fs, tol=None, flags=0):
     """GPU vs oracle within max(cond_tol, 4 x the oracle's own distance from exact arithmetic):
     at cond(K) ~ 1e5..1e7 the reference algorithm itself is only good to ~1e-9 (kernel-parameter
     gradients through the explicit K^{-1} of slogdet's backward rule)."""
     tol = cond_tol(prob, params) if tol is None else tol
-    s = device_solver(prob, Q, fs)
+    s = device_solver(prob, Q, fs, flags=flags)
     s.set_params(params)
     loss, g = s.loss_grad()
     lo, go, errs = oracle_err(prob, params)
@@ -183,3 +183,31 @@ def test_step_deterministic():
         out.append(s.get_flat())
         s.close()
     assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("eq,kind,n1,n2", [("poisson", "Matern52_Cos_1d", 96, 80),
+                                          ("advection", "SE_Cos_1d", 72, 150),
+                                          ("allencahn", "Matern52_1d", 40, 36)])
+def test_loss_grad_2d_big_gemm_path(eq, kind, n1, n2):
+    """The 64x64 throughput GEMM (used from ~1500^2 up, e.g. C5's 4096^2), forced at small
+    sizes: every stage, both operand transposes, dual products, fused epilogues, and 64-tiles
+    half outside the 32-padded matrices (96 and 160 pad to an odd number of 32-blocks)."""
+    from gpk._lib import GPK_FLAG_FORCE_BIG_GEMM
+    prob, params, _, fs = problem_2d(eq=eq, kind=kind, n1=n1, n2=n2, Q=5, seed=7)
+    _cmp_lossgrad(prob, params, 5, fs, flags=GPK_FLAG_FORCE_BIG_GEMM)
+
+
+def test_big_gemm_adam_and_predict_match_small():
+    """Same trajectory and predictions with the big and the small GEMM kernels."""
+    from gpk._lib import GPK_FLAG_FORCE_BIG_GEMM
+    prob, params, (Xte, _), fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=72, n2=56, Q=6, seed=2)
+    out = []
+    for flags in (0, GPK_FLAG_FORCE_BIG_GEMM):
+        s = device_solver(prob, 6, fs, flags=flags)
+        s.set_params(params)
+        losses = s.step(10)
+        out.append((losses, s.get_flat(), s.predict(Xte[0], Xte[1])))
+        s.close()
+    assert rel(out[0][0], out[1][0]) < 1e-11
+    assert rel(out[0][1], out[1][1]) < 1e-9
+    assert rel(out[0][2], out[1][2]) < 1e-10
