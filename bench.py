@@ -32,6 +32,23 @@ METRIC = "log-joint iters/sec + fp64 Cholesky GFLOP/s, 2D Poisson 256^2, 1-8 GPU
 KERNEL_LAUNCHES = {"sweep": None, "gemm_B": 5, "pgrad": 1, "assemble": 1}  # per step (sweep: T)
 
 
+# rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench (tools/gpu_round.sh), summarised by
+# tools/pmc_summary.py: HBM-side bytes per launch (2*FETCH + WRITE, MI355X_MICROARCH.md §HBM)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_pmc_c4.json")
+PMC_KERNEL = {"sweep": "gpk::sweep_kernel", "gemm_B": "gpk::gemm_small_kernel",
+              "pgrad": "gpk::pgrad_kernel<true, true, 2, false>", "assemble": "gpk::assemble_kernel<true, true, 2>"}
+
+
+def pmc_traffic(kernel):
+    """Bytes per launch of `kernel` from the committed PMC summary (None if absent)."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            k = json.load(f)["kernels"].get(kernel)
+        return None if k is None else k["traffic_bytes"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_baseline(config, seconds, max_steps=400):
     """The CPU oracle (oracle/gp_oracle.py: NumPy/SciPy LU + OpenMP C fields) on the same
     workload, bounded sample of `seconds` of work (test infrastructure; never the product)."""
@@ -121,7 +138,7 @@ def main():
         roof = {"kernel": dom, "bound": "mfma", "achieved": d["flops"] / (d["us"] * 1e-6) / 1e12,
                 "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s"}
     roof["frac"] = roof["achieved"] / roof["peak"]
-    roof["traffic"] = None
+    roof["traffic"] = pmc_traffic(PMC_KERNEL[dom])
     roof["avg_launch_us"] = d["us"]
     roof["alg_flops_per_launch"] = d["flops"]
     roof["alg_bytes_per_launch"] = d["bytes"]
