@@ -102,7 +102,9 @@ struct gpk_handle {
   std::vector<GemmDesc> hdescs;  // per-stage GEMM descriptors (kernel arguments)
   Stage st[kGemmStages];
   double *Kc[2] = {}, *pst[2] = {};  // kept K (refinement residuals), pivot stats (gate)
-  unsigned int* aflag[2] = {};        // assembly -> pivot-0 hand-off counters
+  unsigned int* aflag[2] = {};        // assembly -> pivot-0 hand-off counters (small path) /
+                                      // update -> pivot hand-off counters (large path)
+  bool bigspd = false;                // large-factor SPD inverse (spdinv_big.hip)
   double* rvec = nullptr;            // 1D refinement residual
   // predict scratch
   GemmDesc* pdescs = nullptr;
@@ -166,6 +168,29 @@ static PrepArgs make_prep(gpk_handle* h, int apply) {
   return P;
 }
 
+static void fill_spd(gpk_handle* h, SpdArgs* sa) {
+  const Layout& L = h->L;
+  for (int a = 0; a < L.naxes; ++a) {
+    sa[a] = SpdArgs{};
+    sa[a].X = h->K[a];
+    sa[a].Y = h->Kb[a];
+    sa[a].p = a == 0 ? L.p1 : L.p2;
+    sa[a].n = a == 0 ? L.n1 : L.n2;
+    sa[a].piv = h->piv[a];
+    sa[a].ldet = h->ldet[a];
+    sa[a].status = h->status;
+    sa[a].pst = h->pst[a];
+    sa[a].flag = h->aflag[a];
+  }
+}
+
+// the SPD inverse of every factor (small: 32-wide sweeps, pivot 0 possibly fused into the
+// assembly launch; large: 64-wide panel/update sweeps)
+static hipError_t launch_inverse(gpk_handle* h, SpdArgs* sa, double** fin, bool pivot0_done) {
+  if (h->bigspd) return launch_spd_inverse_big(sa, h->L.naxes, fin, h->s);
+  return launch_spd_inverse(sa, h->L.naxes, fin, h->s, pivot0_done);
+}
+
 // assemble K, D (+ step constants, + pivot block 0) and invert K: the first part of a step
 static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
   const Layout& L = h->L;
@@ -181,27 +206,20 @@ static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
     aa[a].D = h->D[a];
     aa[a].deriv = deriv;
     aa[a].Kc = h->Kc[a];
-    aa[a].piv = h->piv[a];
-    aa[a].ldet = h->ldet[a];
-    aa[a].pst = h->pst[a];
-    aa[a].status = h->status;
-    aa[a].flag = h->aflag[a];
+    if (!h->bigspd) {  // pivot block 0 factored inside the assembly launch (small path)
+      aa[a].piv = h->piv[a];
+      aa[a].ldet = h->ldet[a];
+      aa[a].pst = h->pst[a];
+      aa[a].status = h->status;
+      aa[a].flag = h->aflag[a];
+    }
   }
   TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, apply), h->s), "assemble"));
   mark(h, 1);
   SpdArgs sa[2];
-  for (int a = 0; a < L.naxes; ++a) {
-    sa[a].X = h->K[a];
-    sa[a].Y = h->Kb[a];
-    sa[a].p = a == 0 ? L.p1 : L.p2;
-    sa[a].n = a == 0 ? L.n1 : L.n2;
-    sa[a].piv = h->piv[a];
-    sa[a].ldet = h->ldet[a];
-    sa[a].status = h->status;
-    sa[a].pst = h->pst[a];
-  }
+  fill_spd(h, sa);
   double* fin[2] = {nullptr, nullptr};
-  TRY(check_launch(launch_spd_inverse(sa, L.naxes, fin, h->s, true), "spd_inverse"));
+  TRY(check_launch(launch_inverse(h, sa, fin, true), "spd_inverse"));
   for (int a = 0; a < L.naxes; ++a) h->Kinv[a] = fin[a];
   mark(h, 2);
   return GPK_OK;
@@ -633,6 +651,11 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
   h->L = make_layout(p);
   h->hyper = AdamHyper{p->lr, p->b1, p->b2, p->eps};
   const Layout& L = h->L;
+  {
+    const int pmax = std::max(L.p1, L.dim == 2 ? L.p2 : 0);
+    h->bigspd = (p->flags & GPK_FLAG_FORCE_BIG_SPD) != 0 ||
+                (!(p->flags & GPK_FLAG_FORCE_SMALL_SPD) && pmax >= SPD_BIG_MIN);
+  }
   auto bail = [&](int rc) {
     gpk_destroy(h);
     return rc;
@@ -666,7 +689,7 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
     A_(h->K[a], (size_t)P * P);
     A_(h->Kb[a], (size_t)P * P);
     A_(h->D[a], (size_t)P * P);
-    A_(h->piv[a], (size_t)P * 32);
+    A_(h->piv[a], std::max<size_t>((size_t)P * 32, 64 * 64));  // large path: 64x64 L^{-1}
     A_(h->ldet[a], P / 32);
     A_(h->Kc[a], (size_t)P * P);
     A_(h->pst[a], 2);
@@ -721,7 +744,7 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
   // of the inverse into a throwaway capture is unnecessary -- compute it directly.
   for (int a = 0; a < L.naxes; ++a) {
     const int T = (a == 0 ? P1 : P2) / 32;
-    h->Kinv[a] = (T & 1) ? h->Kb[a] : h->K[a];
+    h->Kinv[a] = h->bigspd ? h->K[a] : ((T & 1) ? h->Kb[a] : h->K[a]);
   }
   if (L.dim == 2 && (rc = build_descs(h)) != GPK_OK) return bail(rc);
   *out = h;
@@ -982,14 +1005,10 @@ int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us) {
     }
     TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
     SpdArgs sa[2];
-    for (int a = 0; a < L.naxes; ++a) {
-      sa[a].X = h->K[a]; sa[a].Y = h->Kb[a]; sa[a].p = a == 0 ? L.p1 : L.p2; sa[a].n = a == 0 ? L.n1 : L.n2;
-      sa[a].piv = h->piv[a]; sa[a].ldet = h->ldet[a]; sa[a].status = h->status;
-      sa[a].pst = h->pst[a];
-    }
+    fill_spd(h, sa);
     double* fin[2];
     HIPCHK(hipEventRecord(e0, h->s));
-    TRY(check_launch(launch_spd_inverse(sa, L.naxes, fin, h->s), "spd_inverse"));
+    TRY(check_launch(launch_inverse(h, sa, fin, false), "spd_inverse"));
     HIPCHK(hipEventRecord(e1, h->s));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0.f;
@@ -1141,14 +1160,49 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     aa[a].x = a == 0 ? h->x1 : h->x2; aa[a].n = a == 0 ? L.n1 : L.n2; aa[a].p = a == 0 ? L.p1 : L.p2;
     aa[a].kc = h->kc + a; aa[a].jitter = h->prob.jitter; aa[a].K = h->K[a]; aa[a].D = h->D[a];
     aa[a].deriv = deriv; aa[a].Kc = nullptr;
-    sa[a].X = h->K[a]; sa[a].Y = h->Kb[a]; sa[a].p = aa[a].p; sa[a].n = aa[a].n;
-    sa[a].piv = h->piv[a]; sa[a].ldet = h->ldet[a]; sa[a].status = h->status;
-      sa[a].pst = h->pst[a];
   }
+  fill_spd(h, sa);
   std::function<hipError_t()> launch;
   double flops = 0.0, bytes = 0.0;
   const double n1 = L.n1, n2 = L.dim == 2 ? L.n2 : 0.0;
-  if (nm == "sweep") {
+  if (nm == "sweep" && h->bigspd) {
+    // large path: time the update launch of sweep 0 (in place, so every timed launch gets a
+    // freshly assembled K, pivot 0 and panel 0 first; only the update is between the events)
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    double tot = 0.0;
+    for (int it = 0; it < iters; ++it) {
+      TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
+      TRY(check_launch(launch_spd_big_stage(sa, L.naxes, -1, h->s), "pivot_init"));
+      TRY(check_launch(launch_spd_big_stage(sa, L.naxes, 0, h->s), "panel"));
+      HIPCHK(hipEventRecord(e0, h->s));
+      TRY(check_launch(launch_spd_big_stage(sa, L.naxes, 1, h->s), "update"));
+      HIPCHK(hipEventRecord(e1, h->s));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      tot += ms * 1000.0;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    // n^3 per factor over its ceil(p/64) sweeps; HBM: read + write the lower triangle
+    for (int a = 0; a < L.naxes; ++a) {
+      const double n = a == 0 ? n1 : n2;
+      flops += n * n * n / spd_big_sweeps(a == 0 ? L.p1 : L.p2);
+      bytes += 8.0 * n * n;
+    }
+    *avg_us = tot / iters;
+    *alg_flops = flops;
+    *alg_bytes = bytes;
+    return read_status(h);
+  } else if ((nm == "spd_pivot" || nm == "spd_panel") && h->bigspd) {
+    // large path pieces (idempotent): the 64-pivot factorisation of block 0, the panel of sweep 0
+    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
+    TRY(check_launch(launch_spd_big_stage(sa, L.naxes, -1, h->s), "pivot_init"));
+    const int stage = nm == "spd_pivot" ? -1 : 0;
+    launch = [&, stage]() { return launch_spd_big_stage(sa, L.naxes, stage, h->s); };
+  } else if (nm == "sweep") {
     // re-assemble K and factor pivot 0, then time sweep 0 (idempotent: X -> Y, piv[1]).
     TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
     TRY(check_launch(launch_spd_stage(sa, L.naxes, -1, h->s), "pivot_init"));

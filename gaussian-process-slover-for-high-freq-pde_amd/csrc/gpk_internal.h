@@ -134,12 +134,23 @@ struct SpdArgs {
   double* ldet;    // [p/NB] logdet contribution of each pivot block
   double* pst;     // refinement gate [2]: K_00, bits of max diag K^{-1} (gate_open)
   int* status;     // nonzero => not positive definite
+  unsigned int* flag;  // large path: update -> pivot hand-off counter (zero-initialised)
 };
 // Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.
 // pivot0_done: pivot block 0 was already factored (by the assembly launch).
 hipError_t launch_spd_inverse(SpdArgs* args, int nmat, double** final_out, hipStream_t s,
                               bool pivot0_done = false);
 hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
+
+// Large-factor path (spdinv_big.hip): 64-wide pivots, panel + lower-tile MFMA update per sweep,
+// next pivot factored inside the update launch.  In place: K^{-1} ends in X.  Y is used as the
+// 64 x p panel buffer and piv as the 64 x 64 L^{-1} buffer (p >= 128).
+// Chosen when the largest padded factor is >= SPD_BIG_MIN (or forced by a problem flag).
+constexpr int SPD_BIG_MIN = 768;
+hipError_t launch_spd_inverse_big(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
+// stage -1: pivot 0; 2k: panel of sweep k; 2k+1: update of sweep k
+hipError_t launch_spd_big_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
+int spd_big_sweeps(int p);
 
 // Iterative-refinement gate: a refinement GEMM/GEMV runs only when the factor's condition
 // number may be large.  gate[0] = K_00 = max diagonal of K (written with pivot block 0),

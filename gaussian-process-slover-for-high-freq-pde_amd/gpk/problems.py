@@ -38,7 +38,7 @@ def problem_arrays(cfg):
     return dict(x1=x, x2=x.copy(), src=src(xm, ym) * np.ones_like(xm), bvals=boundary_2d(u(xm, ym)))
 
 
-def make_solver(config, seed=0, device=0, Q=30, lr=0.01, random_u=True):
+def make_solver(config, seed=0, device=0, Q=30, lr=0.01, random_u=True, flags=0):
     """A DeviceSolver for a BASELINE config with U ~ 0.1 N(0,1) (seeded), other params at the
     reference init."""
     cfg = CONFIGS[config] if isinstance(config, str) else config
@@ -48,7 +48,8 @@ def make_solver(config, seed=0, device=0, Q=30, lr=0.01, random_u=True):
           "allencahn_2d": "allencahn", "advection": "advection"}[eq]
     s = DeviceSolver(cfg["dim"], eq, cfg["kernel"], arr["x1"], arr["src"], arr["bvals"],
                      x2=arr.get("x2"), bidx=arr.get("bidx"), Q=Q, llk_weight=cfg["llk_weight"],
-                     beta=cfg.get("beta", 1.0), lr=lr, freq_scale=cfg["freq_scale"], device=device)
+                     beta=cfg.get("beta", 1.0), lr=lr, freq_scale=cfg["freq_scale"], device=device,
+                     flags=flags)
     if random_u:
         flat = s.get_flat()
         rng = np.random.default_rng(seed)

@@ -75,6 +75,8 @@ typedef struct gpk_problem {
 
 /* gpk_problem.flags bits */
 #define GPK_FLAG_FORCE_BIG_GEMM 1 /* use the 64x64 throughput GEMM at every size (tests/tuning) */
+#define GPK_FLAG_FORCE_BIG_SPD 2  /* use the 64-wide panel/update SPD inverse at every size */
+#define GPK_FLAG_FORCE_SMALL_SPD 4 /* use the 32-wide sweep SPD inverse at every size */
 
 typedef struct gpk_handle gpk_handle;
 
