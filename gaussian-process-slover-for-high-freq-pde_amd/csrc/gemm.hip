@@ -430,17 +430,259 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(GemmBatch batch, const St
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Largest-size variant (M, N >= ~2048, e.g. the 4096^2 advection grid): a 128x128 output tile
+// per 256-thread workgroup, each wave a 64x64 quadrant = 4x4 v_mfma_f64_16x16x4 blocks (every
+// LDS fragment feeds 4 MFMAs, 16 independent accumulation chains per wave); 16-deep K-steps
+// through double-buffered LDS ([k][m] / [k][n], rows 144 doubles apart = 32 banks), the next
+// step prefetched global -> registers with 16-B loads that read whole contiguous segments.
+// A dual product is folded into the same accumulators: its A2 operand is scaled by
+// alpha2 / alpha on the way into LDS, and the epilogue applies alpha once.  Tiles are dealt
+// XCD-major and walked in groups of 4 tile rows (A/B panel reuse in each XCD's L2).
+// 128x128 tiles measured 55.9 TF/s on 4096^3 NN vs 40.2 TF/s for the 64x64 kernel
+// (tools/probes/gemm128_probe.hip).
+// ---------------------------------------------------------------------------------------
+namespace huge {
+constexpr int TM = 128, KS = 16, S = 144, GROUP_M = 4;
+
+struct Regs { double2 a[4], b[4]; };
+
+// Branch-free: rows / columns past M, N (edge tiles of a 32-padded matrix) load a clamped,
+// in-bounds address instead.  Those values only reach output rows / columns >= M, N, which are
+// never stored, so no zeroing is needed -- and an unconditional load keeps the K-loop free of
+// divergent control flow (a guarded load becomes an exec-mask branch, and the compiler then
+// shuttles the 128 accumulators between VGPRs and AGPRs every K-step).
+__device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+
+template <int ta, int tb>
+__device__ __forceinline__ void fetch(Regs& R, const double* A, int lda, const double* B, int ldb,
+                                      int M, int N, int i0, int j0, int k0, int t) {
+  if (!ta) {  // A[i][k], k contiguous (16 per tile row): row (t>>3) + 32j, k pair 2(t&7)
+    const int kc = 2 * (t & 7);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = i0 + (t >> 3) + 32 * j;
+      R.a[j] = ld2(A + (size_t)min(r, M - 1) * lda + k0 + kc);
+    }
+  } else {    // A[k][i], i contiguous (128 per tile row): k row (t>>6) + 4j, i pair 2(t&63)
+    const int ic = i0 + 2 * (t & 63);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kr = (t >> 6) + 4 * j;
+      R.a[j] = ld2(A + (size_t)(k0 + kr) * lda + min(ic, M - 2));
+    }
+  }
+  if (!tb) {  // B[k][j], j contiguous
+    const int jc = j0 + 2 * (t & 63);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kr = (t >> 6) + 4 * j;
+      R.b[j] = ld2(B + (size_t)(k0 + kr) * ldb + min(jc, N - 2));
+    }
+  } else {    // B[j][k], k contiguous
+    const int kc = 2 * (t & 7);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = j0 + (t >> 3) + 32 * j;
+      R.b[j] = ld2(B + (size_t)min(r, N - 1) * ldb + k0 + kc);
+    }
+  }
+}
+
+// registers -> LDS ([k][m] and [k][n]); A scaled by sa (the dual product's alpha2 / alpha)
+template <int ta, int tb>
+__device__ __forceinline__ void store(const Regs& R, double* sA, double* sB, double sa, int t) {
+  if (!ta) {
+    const int kc = 2 * (t & 7);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = (t >> 3) + 32 * j;
+      sA[kc * S + r] = sa * R.a[j].x;
+      sA[(kc + 1) * S + r] = sa * R.a[j].y;
+    }
+  } else {
+    const int ic = 2 * (t & 63);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double2 v = {sa * R.a[j].x, sa * R.a[j].y};
+      *reinterpret_cast<double2*>(sA + ((t >> 6) + 4 * j) * S + ic) = v;
+    }
+  }
+  if (!tb) {
+    const int jc = 2 * (t & 63);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<double2*>(sB + ((t >> 6) + 4 * j) * S + jc) = R.b[j];
+  } else {
+    const int kc = 2 * (t & 7);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = (t >> 3) + 32 * j;
+      sB[kc * S + r] = R.b[j].x;
+      sB[(kc + 1) * S + r] = R.b[j].y;
+    }
+  }
+}
+
+__device__ __forceinline__ void mma(const double* sA, const double* sB, int wr, int wc, int lane,
+                                    d4 (&acc)[4][4]) {
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < KS / 4; ++kk) {
+    const int k = 4 * kk + lk;
+    double a[4], b[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      a[x] = sA[k * S + 64 * wr + 16 * x + li];
+      b[x] = sB[k * S + 64 * wc + 16 * x + li];
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+        acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[y], acc[x][y], 0, 0, 0);
+  }
+}
+
+// acc += sa * op(A) op(B) over K (multiple of 16... of 32 by the padding contract)
+template <int ta, int tb>
+__device__ __forceinline__ void product_t(const double* A, int lda, const double* B, int ldb,
+                                          int K, int M, int N, int i0, int j0, double sa, double* sA0,
+                                          double* sB0, int t, int wr, int wc, int lane, d4 (&acc)[4][4]) {
+  constexpr int SZ = KS * S;
+  Regs R;
+  const int nk = K / KS;
+  fetch<ta, tb>(R, A, lda, B, ldb, M, N, i0, j0, 0, t);
+  store<ta, tb>(R, sA0, sB0, sa, t);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) fetch<ta, tb>(R, A, lda, B, ldb, M, N, i0, j0, (kt + 1) * KS, t);
+    mma(sA0 + cur * SZ, sB0 + cur * SZ, wr, wc, lane, acc);
+    if (kt + 1 < nk) store<ta, tb>(R, sA0 + (cur ^ 1) * SZ, sB0 + (cur ^ 1) * SZ, sa, t);
+    __syncthreads();
+  }
+}
+
+}  // namespace huge
+
+// one instantiation per transpose signature of (product, dual product): the K-loops carry no
+// branches at all (a runtime transpose switch makes the compiler shuttle the accumulators
+// between AGPRs and VGPRs every K-step); the launcher splits a batch by signature.
+template <int TA, int TB, int TA2, int TB2>
+__global__ __launch_bounds__(256) void gemm_huge_kernel(GemmBatch batch, const StepScalars* __restrict__ sc,
+                                                        int per_xcd) {
+  using namespace huge;
+  const GemmDesc& d = batch.d[blockIdx.y];
+  const int tm = (d.M + TM - 1) / TM, tn = (d.N + TM - 1) / TM;
+  const int o = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);  // XCD-major dealing
+  if (o >= tm * tn) return;
+  if (!gate_open(d.gate)) return;  // refinement not needed (uniform)
+  const int gsz = GROUP_M * tn, grp = o / gsz, first = grp * GROUP_M;
+  const int gm = min(GROUP_M, tm - first), in = o - grp * gsz;
+  const int ti = first + in % gm, tj = in / gm;
+  const int tile = ti * tn + tj;  // partial-sum slot (row-major tile index)
+  const int i0 = ti * TM, j0 = tj * TM;
+  __shared__ double sA[2 * KS * S], sB[2 * KS * S];
+  __shared__ double sred[4], sred2[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  double alpha = d.alpha, alpha2 = d.alpha2;
+  if (d.vscale) alpha *= sc->v;
+  if (d.vscale2) alpha2 *= sc->v;
+  d4 acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = d4{0.0, 0.0, 0.0, 0.0};
+  product_t<TA, TB>(d.A, d.lda, d.B, d.ldb, d.K, d.M, d.N, i0, j0, 1.0, sA, sB, t, wr, wc, lane, acc);
+  if (d.K2)
+    product_t<TA2, TB2>(d.A2, d.lda2, d.B2, d.ldb2, d.K2, d.M, d.N, i0, j0, alpha2 / alpha, sA, sB, t,
+                        wr, wc, lane, acc);
+  double part = 0.0, part2 = 0.0;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i0 + 64 * wr + 16 * x + (lane >> 4) + 4 * r;
+        const int col = j0 + 64 * wc + 16 * y + (lane & 15);
+        if (row < d.M && col < d.N) {
+          const EpiIn e = epi_fetch(d, row, col);
+          d.C[(size_t)row * d.ldc + col] = epi_apply(d, alpha * acc[x][y][r], e, part, part2);
+        }
+      }
+    asm volatile("" ::: "memory");  // keep the epilogue's operand loads to one row block at a time
+  }
+  if (d.red) {
+    double s = block_sum_256(part, sred);
+    if (t == 0) d.red[tile] = s;
+  }
+  if (d.red2) {
+    double s = block_sum_256(part2, sred2);
+    if (t == 0) d.red2[tile] = s;
+  }
+}
+
+typedef void (*HugeFn)(GemmBatch, const StepScalars*, int);
+static HugeFn huge_fn(int sig) {
+  static const HugeFn tab[16] = {
+      gemm_huge_kernel<0, 0, 0, 0>, gemm_huge_kernel<0, 0, 0, 1>, gemm_huge_kernel<0, 0, 1, 0>,
+      gemm_huge_kernel<0, 0, 1, 1>, gemm_huge_kernel<0, 1, 0, 0>, gemm_huge_kernel<0, 1, 0, 1>,
+      gemm_huge_kernel<0, 1, 1, 0>, gemm_huge_kernel<0, 1, 1, 1>, gemm_huge_kernel<1, 0, 0, 0>,
+      gemm_huge_kernel<1, 0, 0, 1>, gemm_huge_kernel<1, 0, 1, 0>, gemm_huge_kernel<1, 0, 1, 1>,
+      gemm_huge_kernel<1, 1, 0, 0>, gemm_huge_kernel<1, 1, 0, 1>, gemm_huge_kernel<1, 1, 1, 0>,
+      gemm_huge_kernel<1, 1, 1, 1>};
+  return tab[sig & 15];
+}
+static int huge_sig(const GemmDesc& d) {
+  const int ta2 = d.K2 ? d.ta2 : 0, tb2 = d.K2 ? d.tb2 : 0;
+  return (d.ta ? 8 : 0) | (d.tb ? 4 : 0) | (ta2 ? 2 : 0) | (tb2 ? 1 : 0);
+}
+
+// one launch per transpose signature present in the batch
+static hipError_t launch_huge(const GemmDesc* descs, int ndesc, const StepScalars* sc, hipStream_t s) {
+  bool done[GEMM_MAX_BATCH] = {};
+  for (int i = 0; i < ndesc; ++i) {
+    if (done[i]) continue;
+    const int sig = huge_sig(descs[i]);
+    GemmBatch b{};
+    int nb = 0, mt = 0;
+    for (int j = i; j < ndesc; ++j)
+      if (!done[j] && huge_sig(descs[j]) == sig) {
+        done[j] = true;
+        b.d[nb++] = descs[j];
+        mt = std::max(mt, gemm_tiles(descs[j], GEMM_HUGE));
+      }
+    const int per = (mt + 7) / 8;
+    hipLaunchKernelGGL(huge_fn(sig), dim3(8 * per, nb), dim3(256), 0, s, b, sc, per);
+  }
+  return hipGetLastError();
+}
+
 int gemm_tiles(const GemmDesc& d, int variant) {
   if (variant == GEMM_SMALL) return (d.M / 16) * (d.N / 16);
+  if (variant == GEMM_HUGE) return ((d.M + 127) / 128) * ((d.N + 127) / 128);
   if (variant == GEMM_BIG) return ((d.M + 63) / 64) * ((d.N + 63) / 64);
   return (d.M / 32) * (d.N / 32);
 }
 
 int gemm_variant(const GemmDesc* descs, int ndesc, int force_big) {
+  if (force_big == 2) {
+    for (int i = 0; i < ndesc; ++i)
+      if (descs[i].K2 && descs[i].alpha == 0.0) return GEMM_BIG;
+    return GEMM_HUGE;
+  }
   if (force_big) return GEMM_BIG;
-  long tot16 = 0;
-  for (int i = 0; i < ndesc; ++i) tot16 += (long)(descs[i].M / 16) * (descs[i].N / 16);
-  return gemm_use_small(tot16) ? GEMM_SMALL : GEMM_BIG;
+  long tot16 = 0, tot128 = 0;
+  for (int i = 0; i < ndesc; ++i) {
+    tot16 += (long)(descs[i].M / 16) * (descs[i].N / 16);
+    tot128 += (long)((descs[i].M + 127) / 128) * ((descs[i].N + 127) / 128);
+  }
+  if (gemm_use_small(tot16)) return GEMM_SMALL;
+  for (int i = 0; i < ndesc; ++i)  // the 128x128 kernel folds a dual product by alpha2 / alpha
+    if (descs[i].K2 && descs[i].alpha == 0.0) return GEMM_BIG;
+  return tot128 >= GEMM_HUGE_MIN_TILES ? GEMM_HUGE : GEMM_BIG;
 }
 
 hipError_t launch_gemm_auto(const GemmDesc* descs, int ndesc, const StepScalars* sc, hipStream_t s,
@@ -457,6 +699,8 @@ hipError_t launch_gemm_auto(const GemmDesc* descs, int ndesc, const StepScalars*
   } else if (variant == GEMM_BIG) {
     const int per = (mt + 7) / 8;
     hipLaunchKernelGGL(gemm_big_kernel, dim3(8 * per, ndesc), dim3(256), 0, s, b, sc, per);
+  } else if (variant == GEMM_HUGE) {
+    return launch_huge(descs, ndesc, sc, s);
   } else {
     hipLaunchKernelGGL(gemm_kernel, dim3(mt, ndesc), dim3(256), 0, s, b, sc);
   }

@@ -325,6 +325,10 @@ static int enqueue_step(gpk_handle* h, int apply) {
   return GPK_OK;
 }
 
+static int gemm_force(int flags) {
+  return (flags & GPK_FLAG_FORCE_HUGE_GEMM) ? 2 : (flags & GPK_FLAG_FORCE_BIG_GEMM) ? 1 : 0;
+}
+
 static int build_descs(gpk_handle* h) {
   const Layout& L = h->L;
   const int P1 = L.p1, P2 = L.p2;
@@ -339,7 +343,7 @@ static int build_descs(gpk_handle* h) {
     return g;
   };
   auto begin = [&](int k) { h->st[k].off = (int)d.size(); };
-  const int force_big = (h->prob.flags & GPK_FLAG_FORCE_BIG_GEMM) ? 1 : 0;
+  const int force_big = gemm_force(h->prob.flags);
   auto end = [&](int k) {
     h->st[k].n = (int)d.size() - h->st[k].off;
     h->st[k].variant = gemm_variant(d.data() + h->st[k].off, h->st[k].n, force_big);
@@ -936,7 +940,7 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
     d[5].beta = 1.0; d[5].C0 = Sw; d[5].ldc0 = P2;
     mk(d[6], Kmn1, P1, 0, Sw, P2, 0, Mw, P2, M1p, P2, P1);
     mk(d[7], Mw, P2, 0, Kmn2, P2, 1, res, M2p, M1p, M2p, P2);
-    const int force_big = (h->prob.flags & GPK_FLAG_FORCE_BIG_GEMM) ? 1 : 0;
+    const int force_big = gemm_force(h->prob.flags);
     for (int k = 0; k < 8; ++k)
       (void)launch_gemm_auto(d + k, 1, h->sc, h->s, gemm_variant(d + k, 1, force_big));
     for (int i = 0; i < m1; ++i)
@@ -1123,7 +1127,7 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
     }
     g.C = tmp; g.ldc = P2; g.M = P1; g.N = P2; g.alpha = 1.0; g.epi = EPI_STORE;
     hipError_t e = launch_gemm_auto(&g, 1, h->sc, h->s,
-                                    gemm_variant(&g, 1, (h->prob.flags & GPK_FLAG_FORCE_BIG_GEMM) ? 1 : 0));
+                                    gemm_variant(&g, 1, gemm_force(h->prob.flags)));
     if (e != hipSuccess) { cleanup(); return fail(GPK_EHIP, hipGetErrorString(e)); }
     src = tmp;
   }

@@ -146,7 +146,7 @@ hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
 // next pivot factored inside the update launch.  In place: K^{-1} ends in X.  Y is used as the
 // 64 x p panel buffer and piv as the 64 x 64 L^{-1} buffer (p >= 128).
 // Chosen when the largest padded factor is >= SPD_BIG_MIN (or forced by a problem flag).
-constexpr int SPD_BIG_MIN = 768;
+constexpr int SPD_BIG_MIN = 1600;
 hipError_t launch_spd_inverse_big(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
 // stage -1: pivot 0; 2k: panel of sweep k; 2k+1: update of sweep k
 hipError_t launch_spd_big_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
@@ -192,8 +192,11 @@ hipError_t launch_gemm_batch(const GemmDesc* descs, int ndesc, int max_tiles,
                              const StepScalars* sc, hipStream_t s, int small);
 // heuristic: use the 16x16 latency kernel while the whole stage has few enough tiles
 inline bool gemm_use_small(long tiles16_total) { return tiles16_total <= 16384; }
-enum { GEMM_TILED32 = 0, GEMM_SMALL = 1, GEMM_BIG = 2 };
-// variant for a batch (force_big: the 64x64 throughput kernel regardless of size), tiles of a
+enum { GEMM_TILED32 = 0, GEMM_SMALL = 1, GEMM_BIG = 2, GEMM_HUGE = 3 };
+// 128x128 tiles once a launch has this many of them (one round over the 256 CUs)
+constexpr long GEMM_HUGE_MIN_TILES = 256;
+// variant for a batch (force_big 1: the 64x64 throughput kernel, 2: the 128x128 one, regardless
+// of size), tiles of a
 // descriptor under a variant (= the entries its red/red2 partials fill), and the launcher
 int gemm_variant(const GemmDesc* descs, int ndesc, int force_big);
 int gemm_tiles(const GemmDesc& d, int variant);

@@ -15,6 +15,7 @@ GPK_OK, GPK_EINVAL, GPK_ENOTPD, GPK_EHIP, GPK_ERCCL, GPK_ENOMEM, GPK_ENODEV = ra
 GPK_FLAG_FORCE_BIG_GEMM = 1  # include/gpk.h
 GPK_FLAG_FORCE_BIG_SPD = 2
 GPK_FLAG_FORCE_SMALL_SPD = 4
+GPK_FLAG_FORCE_HUGE_GEMM = 8
 KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}
 EQ_IDS = {"poisson": 0, "allencahn": 1, "advection": 2}
 

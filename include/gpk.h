@@ -77,6 +77,7 @@ typedef struct gpk_problem {
 #define GPK_FLAG_FORCE_BIG_GEMM 1 /* use the 64x64 throughput GEMM at every size (tests/tuning) */
 #define GPK_FLAG_FORCE_BIG_SPD 2  /* use the 64-wide panel/update SPD inverse at every size */
 #define GPK_FLAG_FORCE_SMALL_SPD 4 /* use the 32-wide sweep SPD inverse at every size */
+#define GPK_FLAG_FORCE_HUGE_GEMM 8 /* use the 128x128 throughput GEMM at every size (tests/tuning) */
 
 typedef struct gpk_handle gpk_handle;
 

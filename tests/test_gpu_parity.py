@@ -190,32 +190,37 @@ def test_step_deterministic():
     assert np.array_equal(out[0], out[1])
 
 
+@pytest.mark.parametrize("variant", ["big", "huge"])
 @pytest.mark.parametrize("eq,kind,n1,n2", [("poisson", "Matern52_Cos_1d", 96, 80),
                                           ("advection", "SE_Cos_1d", 72, 150),
-                                          ("allencahn", "Matern52_1d", 40, 36)])
-def test_loss_grad_2d_big_gemm_path(eq, kind, n1, n2):
-    """The 64x64 throughput GEMM (used from ~1500^2 up, e.g. C5's 4096^2), forced at small
-    sizes: every stage, both operand transposes, dual products, fused epilogues, and 64-tiles
-    half outside the 32-padded matrices (96 and 160 pad to an odd number of 32-blocks)."""
-    from gpk._lib import GPK_FLAG_FORCE_BIG_GEMM
+                                          ("allencahn", "Matern52_1d", 40, 36),
+                                          ("advection", "Matern52_Cos_1d", 136, 200)])
+def test_loss_grad_2d_big_gemm_path(eq, kind, n1, n2, variant):
+    """The 64x64 (big) and 128x128 (huge) throughput GEMMs (used from ~1500^2 / ~2048^2 up,
+    e.g. C5's 4096^2), forced at small sizes: every stage, all transpose signatures (one
+    launch per signature for huge), dual products (folded by alpha2/alpha for huge), fused
+    epilogues, and tiles partly outside the 32-padded matrices (clamped loads)."""
+    from gpk._lib import GPK_FLAG_FORCE_BIG_GEMM, GPK_FLAG_FORCE_HUGE_GEMM
+    flags = GPK_FLAG_FORCE_BIG_GEMM if variant == "big" else GPK_FLAG_FORCE_HUGE_GEMM
     prob, params, _, fs = problem_2d(eq=eq, kind=kind, n1=n1, n2=n2, Q=5, seed=7)
-    _cmp_lossgrad(prob, params, 5, fs, flags=GPK_FLAG_FORCE_BIG_GEMM)
+    _cmp_lossgrad(prob, params, 5, fs, flags=flags)
 
 
 def test_big_gemm_adam_and_predict_match_small():
     """Same trajectory and predictions with the big and the small GEMM kernels."""
-    from gpk._lib import GPK_FLAG_FORCE_BIG_GEMM
+    from gpk._lib import GPK_FLAG_FORCE_BIG_GEMM, GPK_FLAG_FORCE_HUGE_GEMM
     prob, params, (Xte, _), fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=72, n2=56, Q=6, seed=2)
     out = []
-    for flags in (0, GPK_FLAG_FORCE_BIG_GEMM):
+    for flags in (0, GPK_FLAG_FORCE_BIG_GEMM, GPK_FLAG_FORCE_HUGE_GEMM):
         s = device_solver(prob, 6, fs, flags=flags)
         s.set_params(params)
         losses = s.step(10)
         out.append((losses, s.get_flat(), s.predict(Xte[0], Xte[1])))
         s.close()
-    assert rel(out[0][0], out[1][0]) < 1e-11
-    assert rel(out[0][1], out[1][1]) < 1e-9
-    assert rel(out[0][2], out[1][2]) < 1e-10
+    for o in out[1:]:
+        assert rel(out[0][0], o[0]) < 1e-11
+        assert rel(out[0][1], o[1]) < 1e-9
+        assert rel(out[0][2], o[2]) < 1e-10
 
 
 @pytest.mark.parametrize("dim,eq,kind,n1,n2", [(1, "poisson", "Matern52_Cos_1d", 200, 0),
