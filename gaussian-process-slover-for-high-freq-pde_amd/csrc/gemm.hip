@@ -729,7 +729,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvDesc d) {
     if (d.epi == EPI_RESID) {
       y -= d.F[row];
       if (d.ac) {
-        const double u = d.U[row];
+        const double u = d.U[row] + (d.U0 ? d.U0[row] : 0.0);
         y += u * (u * u - 1.0);
       }
       part = y * y;

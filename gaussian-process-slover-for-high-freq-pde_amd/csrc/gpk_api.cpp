@@ -106,6 +106,7 @@ struct gpk_handle {
                                       // update -> pivot hand-off counters (large path)
   bool bigspd = false;                // large-factor SPD inverse (spdinv_big.hip)
   double* rvec = nullptr;            // 1D refinement residual
+  double* uoff = nullptr;            // 1D Allen-Cahn offset (gpk_problem.uoff), or null
   // predict scratch
   GemmDesc* pdescs = nullptr;
 
@@ -246,7 +247,7 @@ static TailArgs make_tail(gpk_handle* h, int apply) {
   au.sc = h->sc; au.Up = h->Up; au.bvals = h->bvals; au.bidx = h->bidx; au.nb = h->prob.nb;
   au.params = h->params; au.grad = h->grad; au.m = h->m; au.v = h->v;
   if (L.dim == 2) { au.S = h->S; au.X1 = h->X1; au.X2 = h->X2; au.R = h->R; }
-  else { au.S = nullptr; au.X1 = h->alpha; au.X2 = h->beta; au.R = h->R; }
+  else { au.S = nullptr; au.X1 = h->alpha; au.X2 = h->beta; au.R = h->R; au.U0 = h->uoff; }
   T.gcount = h->tcount; T.top = h->ttop; T.gpart = h->tgpart; T.pg = h->pg;
   T.tg = h->ttg; T.ngpa = h->tngpa;
   return T;
@@ -285,7 +286,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
     // every K^{-1} application gets one step of iterative refinement x += K^{-1}(b - K x),
     // gated on a cond(K) lower bound (gemv skips itself when K is well conditioned)
     GemvDesc g{};
-    g.lda = P; g.p = P; g.rows = P; g.alpha = 1.0; g.ac = ac; g.F = h->F; g.U = h->Up;
+    g.lda = P; g.p = P; g.rows = P; g.alpha = 1.0; g.ac = ac; g.F = h->F; g.U = h->Up; g.U0 = h->uoff;
     auto gemv = [&](const double* A, const double* x, double* y, double alpha, const double* C0,
                     double beta, int epi, double* red, bool gated) -> int {
       GemvDesc q = g;
@@ -649,6 +650,7 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
   h->prob = *p;
   h->prob.x1 = h->prob.x2 = h->prob.src = h->prob.bvals = nullptr;
   h->prob.bidx = nullptr;
+  h->prob.uoff = nullptr;
   if (p->dim == 2) h->prob.nb = 2 * p->n1 + 2 * p->n2;
   h->freq_scale = freq_scale;
   h->dev = p->device;
@@ -712,6 +714,7 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
     h->nquad = h->negap = (P1 / 16) * (P2 / 16);  // upper bound (16x16 tiles); set in build_descs
   } else {
     A_(h->alpha, P1); A_(h->R, P1); A_(h->tvec, P1); A_(h->beta, P1); A_(h->rvec, P1);
+    if (p->uoff) A_(h->uoff, P1);
     h->nquad = h->negap = gemv_blocks(P1);
   }
   A_(h->red_quad, h->nquad);
@@ -737,6 +740,8 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
   } else {
     (void)hipMemcpyAsync(h->F, p->src, L.n1 * sizeof(double), hipMemcpyHostToDevice, h->s);
     (void)hipMemcpyAsync(h->bidx, p->bidx, p->nb * sizeof(int), hipMemcpyHostToDevice, h->s);
+    if (p->uoff)
+      (void)hipMemcpyAsync(h->uoff, p->uoff, L.n1 * sizeof(double), hipMemcpyHostToDevice, h->s);
   }
   (void)hipMemcpyAsync(h->bvals, p->bvals, h->prob.nb * sizeof(double), hipMemcpyHostToDevice, h->s);
   std::vector<double> init = init_params(p, L, freq_scale);

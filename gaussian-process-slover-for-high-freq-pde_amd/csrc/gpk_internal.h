@@ -218,6 +218,7 @@ struct GemvDesc {
   int epi;           // EPI_STORE / EPI_RESID / EPI_QUAD
   int ac;
   const double* F; const double* U;
+  const double* U0;  // Allen-Cahn offset: the term uses U + U0 (nullable)
   double* red;       // per-block partials
   double* red2; const double* Q1; const double* Q2;  // per-block partials of sum Q1*Q2
   const double* gate; int ngate;

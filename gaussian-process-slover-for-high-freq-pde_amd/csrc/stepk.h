@@ -48,6 +48,7 @@ struct AdamUArgs {
   // 2D: gU = S + v (X1 + X2) (X1 includes beta for advection); 1D: gu = X1 + v X2 (alpha, beta)
   const double* S; const double* X1; const double* X2; const double* R;
   double* Up;
+  const double* U0;  // 1D Allen-Cahn offset (extra-GP second phase), nullable
   const double* bvals;
   const int* bidx; int nb;
   double* params; double* grad; double* m; double* v;

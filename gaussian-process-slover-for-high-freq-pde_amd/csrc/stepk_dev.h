@@ -110,7 +110,10 @@ __device__ __forceinline__ void adam_u_elem(const AdamUArgs& A, int e) {
     pi = e;
     u = A.Up[pi];
     g = A.X1[pi] + v * A.X2[pi];  // alpha + v*beta
-    if (A.ac) g += v * (3.0 * u * u - 1.0) * A.R[pi];
+    if (A.ac) {
+      const double ua = u + (A.U0 ? A.U0[pi] : 0.0);
+      g += v * (3.0 * ua * ua - 1.0) * A.R[pi];
+    }
     for (int k = 0; k < A.nb; ++k)
       if (A.bidx[k] == e) g += wt * (u - A.bvals[k]);
   }

@@ -44,6 +44,7 @@ class gpk_problem(ctypes.Structure):
         ("lr", ctypes.c_double), ("b1", ctypes.c_double), ("b2", ctypes.c_double),
         ("eps", ctypes.c_double),
         ("device", ctypes.c_int32), ("flags", ctypes.c_int32),
+        ("uoff", _dp),
     ]
 
 

@@ -51,7 +51,7 @@ def params_template(dim, n1, n2, Q):
 class DeviceSolver:
     def __init__(self, dim, eq, kind, x1, src, bvals, x2=None, bidx=None, Q=30, jitter=1e-6,
                  llk_weight=200.0, logdet=True, beta=1.0, lr=0.01, freq_scale=20.0, device=0,
-                 b1=0.9, b2=0.999, eps=1e-8, flags=0):
+                 b1=0.9, b2=0.999, eps=1e-8, flags=0, uoff=None):
         lib = _lib.load()
         self.dim = int(dim)
         self.eq = eq
@@ -85,6 +85,13 @@ class DeviceSolver:
         p.lr, p.b1, p.b2, p.eps = lr, b1, b2, eps
         p.device = device
         p.flags = int(flags)
+        if uoff is not None:  # 1D Allen-Cahn offset (extra-GP second phase)
+            if dim != 1:
+                raise ValueError("uoff is a 1D (extra-GP) option")
+            self._uoff = f64(uoff).reshape(-1)
+            if self._uoff.size != self.n1:
+                raise ValueError("uoff must have n1 entries")
+            p.uoff = dptr(self._uoff)
         self._prob = p
         h = ctypes.c_void_p()
         check(lib.gpk_create(ctypes.byref(p), float(freq_scale), ctypes.byref(h)))

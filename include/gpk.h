@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GPK_ABI_VERSION 1
+#define GPK_ABI_VERSION 2  /* 2: gpk_problem.uoff (extra-GP second phase) */
 
 /* status codes */
 enum {
@@ -71,6 +71,10 @@ typedef struct gpk_problem {
   double lr, b1, b2, eps; /* optax.adam(lr) defaults b1=.9, b2=.999, eps=1e-8 */
   int32_t device;       /* HIP device ordinal */
   int32_t flags;        /* GPK_FLAG_* bits, normally 0 */
+  /* dim 1 only, nullable [n1]: a frozen field u0 added to u inside the Allen-Cahn term,
+   * (u+u0)((u+u0)^2-1) -- the extra GP's second phase, where the first GP's u is frozen
+   * (model_GP_solver_1d_extra.py:86-98).  Its u_xx and u0[Xind] enter as shifted src / bvals. */
+  const double* uoff;
 } gpk_problem;
 
 /* gpk_problem.flags bits */

@@ -407,6 +407,100 @@ def criterion_1d(prob, params):
 
 
 # ----------------------------------------------------------------------------------------
+# 1D extra-GP second phase: code/model_GP_solver_1d_extra.py:57-193
+# ----------------------------------------------------------------------------------------
+def _extra_kp(kp):
+    """The extra GP's kernel_paras {log-w, log-ls} (no 'freq': Matern52_1d / SE_1d)."""
+    out = {"log-w": np.asarray(kp["log-w"], np.float64).reshape(-1),
+           "log-ls": np.asarray(kp["log-ls"], np.float64).reshape(-1)}
+    out["freq"] = np.zeros_like(out["log-w"])
+    return out
+
+
+def frozen_fields_1d(prob, params):
+    """(u, u_xx) of the first GP (value_and_grad_kernel, model_GP_solver_1d.py:80-99)."""
+    x = np.asarray(prob["x"], np.float64).reshape(-1)
+    kp = params["kernel_paras"]
+    u = np.asarray(params["u"], np.float64).reshape(-1)
+    K, D = kernel_kd(prob["kind"], x, kp, prob["jitter"], 2)
+    return u, D @ _solve(_lu(K), u)
+
+
+def loss_grad_1d_extra(prob, params, params_extra, kind_extra, want_grad=True):
+    """loss_extra (code/model_GP_solver_1d_extra.py:101-137) and its gradient w.r.t.
+    params_extra: the first GP (prob['kind'], params) frozen, the extra GP (kind_extra,
+    params_extra = {log_tau, log_v, kernel_paras{log-w, log-ls}, u [N,1]})."""
+    x = np.asarray(prob["x"], np.float64).reshape(-1)
+    N = x.size
+    u, uxx = frozen_fields_1d(prob, params)                                  # :106-108
+    ue = np.asarray(params_extra["u"], np.float64).reshape(N, -1).sum(axis=1)  # :111 (sum over trick)
+    log_tau = float(params_extra["log_tau"])
+    log_v = float(params_extra["log_v"])
+    tau, v = math.exp(log_tau), math.exp(log_v)
+    kp = _extra_kp(params_extra["kernel_paras"])
+    wb, c = float(prob["llk_weight"]), float(prob["logdet"])
+    xind = np.asarray(prob["xind"]).reshape(-1)
+    yb = np.asarray(prob["y"], np.float64).reshape(-1)
+    f = np.asarray(prob["src"], np.float64).reshape(-1)
+    Ke, De = kernel_kd(kind_extra, x, kp, prob["jitter"], 2)                   # :64-73
+    lu = _lu(Ke)
+    alpha = _solve(lu, ue)
+    uexx = De @ alpha                                                         # :74-75
+    bres = u[xind] + ue[xind] - yb                                            # :83-85
+    bgap = float(bres @ bres)
+    us = u + ue
+    R = uxx + uexx - f                                                        # :88-90
+    if prob["eq"] == "allencahn":
+        R = uxx + uexx + us * (us * us - 1.0) - f                             # :93-97
+    egap = float(R @ R)
+    log_prior = -0.5 * _slogdet_from_lu(lu) * c - 0.5 * float(ue @ alpha)     # :121-123
+    log_b = 0.5 * xind.size * log_tau - 0.5 * tau * bgap                      # :126-128
+    eq_ll = 0.5 * N * log_v - 0.5 * v * egap                                  # :132-133
+    loss = -(log_prior + log_b * wb + eq_ll)                                  # :135-136
+    if not want_grad:
+        return loss, None
+    beta = _solve(lu, De.T @ R)
+    Kinv = _solve(lu, np.eye(N))
+    GK = 0.5 * c * Kinv - 0.5 * np.outer(alpha, alpha) - v * np.outer(beta, alpha)
+    GD = v * np.outer(R, alpha)
+    gu = alpha + v * beta
+    if prob["eq"] == "allencahn":
+        gu = gu + v * (3.0 * us * us - 1.0) * R
+    np.add.at(gu, xind, wb * tau * bres)
+    gkp = param_grad_contract(kind_extra, x, kp, GK, GD, 2)
+    grad = {"kernel_paras": {"log-w": gkp["log-w"], "log-ls": gkp["log-ls"]},
+            "log_tau": wb * (-0.5 * xind.size + 0.5 * tau * bgap),
+            "log_v": -0.5 * N + 0.5 * v * egap,
+            "u": gu.reshape(np.shape(params_extra["u"]))}
+    return loss, grad
+
+
+def preds_1d_extra(prob, params, params_extra, kind_extra, xte):
+    """preds_extra (code/model_GP_solver_1d_extra.py:148-178): first GP + extra GP."""
+    pe = preds_1d(dict(prob, kind=kind_extra),
+                  {"kernel_paras": _extra_kp(params_extra["kernel_paras"]),
+                   "u": np.asarray(params_extra["u"]).reshape(np.size(prob["x"]), -1).sum(axis=1)}, xte)
+    return preds_1d(prob, params, xte) + pe
+
+
+def criterion_1d_extra(prob, params, params_extra, kind_extra):
+    """compute_early_stopping_extra (code/model_GP_solver_1d_extra.py:180-193)."""
+    x = np.asarray(prob["x"], np.float64).reshape(-1)
+    u, uxx = frozen_fields_1d(prob, params)
+    kp = _extra_kp(params_extra["kernel_paras"])
+    ue = np.asarray(params_extra["u"], np.float64).reshape(-1)
+    Ke, De = kernel_kd(kind_extra, x, kp, prob["jitter"], 2)
+    uexx = De @ _solve(_lu(Ke), ue)
+    xind = np.asarray(prob["xind"]).reshape(-1)
+    bres = u[xind] + ue[xind] - np.asarray(prob["y"]).reshape(-1)
+    R = uxx + uexx - np.asarray(prob["src"]).reshape(-1)
+    if prob["eq"] == "allencahn":
+        us = u + ue
+        R = R + us * (us * us - 1.0)
+    return float(bres @ bres) / xind.size + float(R @ R) / x.size
+
+
+# ----------------------------------------------------------------------------------------
 # 2D Kronecker log-joint: code/model_GP_solver_2d.py:87-183, advection :87-179
 # ----------------------------------------------------------------------------------------
 def boundary_2d(U):
@@ -748,3 +842,53 @@ def train_replay(dim, prob, params, lr, nepoch, test, record_every=None):
             rec["epoch_list"].append(i)
     rec["min_err"] = min_err
     return params, state, rec
+
+
+def train_replay_extra(prob, kind_extra, Q, freq_scale, lr, nepoch, change_point, test, tol=-1.0):
+    """Replays GP_solver_1d_extra.train (code/model_GP_solver_1d_extra.py:195-339): phase-1
+    steps of the single GP while i <= change_point*nepoch, then the extra GP from the frozen
+    params; records every nepoch/20 (at i == change_point the reference evaluates preds_extra
+    on the FIRST GP's params: reproduced), early stop on criterion < tol or 8 error increases."""
+    cp = int(nepoch * change_point)
+    params = init_params_1d(np.size(prob["x"]), Q, freq_scale)
+    opt = Adam(lr)
+    state = opt.init(params)
+    pe = st_e = None
+    rec = {"loss_list": [], "err_list": [], "epoch_list": []}
+    min_err, inc = 2.0, 0
+    every = nepoch / 20
+    extra_pred = False
+    for i in range(nepoch):
+        if i <= cp:
+            loss, g = loss_grad_1d(prob, params)
+            params, state = opt.update(g, state, params)
+        else:
+            loss, g = loss_grad_1d_extra(prob, params, pe, kind_extra)
+            pe, st_e = opt_e.update(g, st_e, pe)
+        if i == cp:
+            pe = {"log_tau": params["log_tau"], "log_v": 0.0,
+                  "kernel_paras": {"log-w": np.zeros(1), "log-ls": np.zeros(1)},
+                  "u": np.zeros((np.size(prob["x"]), 1))}
+            opt_e = Adam(lr)
+            st_e = opt_e.init(pe)
+            extra_pred = True
+        if i % every == 0:
+            cur = params if i <= cp else pe
+            if extra_pred:
+                pred = preds_1d_extra(prob, params, cur, kind_extra, test[0])
+            else:
+                pred = preds_1d(prob, cur, test[0])
+            ute = np.asarray(test[1]).reshape(-1)
+            err = np.linalg.norm(pred.reshape(-1) - ute) / np.linalg.norm(ute)
+            if err < min_err:
+                min_err = err
+            elif err - min_err > 1e-3:
+                inc += 1
+            rec["loss_list"].append(math.log(loss) if loss > 1 else loss)
+            rec["err_list"].append(err)
+            rec["epoch_list"].append(i)
+            crit = criterion_1d(prob, params)
+            if i > 0 and (crit < tol or inc > 7):
+                break
+    rec["min_err"] = min_err
+    return params, pe, rec

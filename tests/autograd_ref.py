@@ -125,3 +125,36 @@ def loss_grad_1d(prob, params):
     loss = -(log_prior + log_b * prob["llk_weight"] + eq_ll)
     loss.backward()
     return float(loss), _grads(tp)
+
+
+def loss_grad_1d_extra(prob, params, params_extra, kind_extra):
+    """loss_extra (code/model_GP_solver_1d_extra.py:101-137) transcribed literally, reverse-mode
+    gradient w.r.t. params_extra (the first GP is evaluated but not differentiated)."""
+    x = torch.tensor(prob["x"])
+    with torch.no_grad():
+        kp0 = {k: torch.tensor(np.asarray(v, np.float64)) for k, v in params["kernel_paras"].items()}
+    u0 = torch.tensor(np.asarray(params["u"], np.float64).reshape(-1, 1))
+    K0, D0 = mats(prob["kind"], x, kp0, prob["jitter"], 2)
+    u_xx = (D0 @ torch.linalg.solve(K0, u0)).detach()
+    tp = _tp(params_extra)
+    kpe = dict(tp["kernel_paras"])
+    kpe["freq"] = torch.zeros_like(kpe["log-w"])
+    u_extra = tp["u"].sum(axis=1).reshape(-1, 1)
+    Ke, De = mats(kind_extra, x, kpe, prob["jitter"], 2)
+    Kinv_u_extra = torch.linalg.solve(Ke, u_extra)
+    u_xx_extra = De @ Kinv_u_extra
+    xind = torch.tensor(np.asarray(prob["xind"]))
+    y = torch.tensor(prob["y"])
+    boundary_gap = ((u0[xind].reshape(-1) + u_extra[xind].reshape(-1) - y.reshape(-1)) ** 2).sum()
+    f = torch.tensor(prob["src"]).reshape(-1)
+    if prob["eq"] == "allencahn":
+        u = u0 + u_extra
+        eq_gap = ((u_xx.flatten() + u_xx_extra.flatten() + (u * (u ** 2 - 1)).flatten() - f) ** 2).sum()
+    else:
+        eq_gap = ((u_xx.flatten() + u_xx_extra.flatten() - f) ** 2).sum()
+    log_prior = -0.5 * torch.linalg.slogdet(Ke)[1] * prob["logdet"] - 0.5 * (u_extra * Kinv_u_extra).sum()
+    log_boundary_ll = 0.5 * xind.numel() * tp["log_tau"] - 0.5 * torch.exp(tp["log_tau"]) * boundary_gap
+    eq_ll = 0.5 * x.numel() * tp["log_v"] - 0.5 * torch.exp(tp["log_v"]) * eq_gap
+    loss = -(log_prior + log_boundary_ll * prob["llk_weight"] + eq_ll)
+    loss.backward()
+    return float(loss), _grads(tp)

@@ -51,3 +51,10 @@ def device_solver(prob, Q, fs=20.0, lr=0.01, flags=0):
 def rel(a, b):
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def extra_params(rng, n):
+    """Seeded extra-GP params (model_GP_solver_1d_extra.py:317-328 shapes, perturbed)."""
+    return {"log_tau": 0.1, "log_v": -0.2,
+            "kernel_paras": {"log-w": 0.2 * rng.normal(size=1), "log-ls": 0.2 * rng.normal(size=1)},
+            "u": 0.05 * rng.normal(size=(n, 1))}

@@ -74,7 +74,7 @@ def test_problem_struct_layout_matches_header(tmp_path):
 def test_abi_version_and_error_channel():
     from gpk import _lib
     lib = _lib.load()
-    assert lib.gpk_abi_version() == 1
+    assert lib.gpk_abi_version() == 2
     assert isinstance(lib.gpk_last_error(), bytes)
     # argument validation happens before any device work
     rc = lib.gpk_create(None, 20.0, None)

@@ -262,3 +262,60 @@ def test_loss_grad_1d_c2_size():
     natural size, against the LU oracle within the cond(K)-scaled budget."""
     prob, params, _ = problem_1d(n=2048, Q=30, seed=6)
     _cmp_lossgrad(prob, params, 30, 20.0, extended=False)
+
+
+def _extra_model(eq, kind, n, Q, nepoch=40, change_point=0.5, n_test=50):
+    from gpk.kernel_matrix import kernel_class
+    from gpk.model_GP_solver_1d_extra import GP_solver_1d_extra
+    name = {"poisson": "poisson_1d-mix_sin", "allencahn": "allencahn_1d-single_sin"}[eq]
+    prob, Xte, Yte = O.setup_1d(name, n, 1.0 if eq == "poisson" else 2 * np.pi, kind, m_test=n_test)
+    tp = {"equation": name, "kernel": kernel_class(kind), "kernel_extra": kernel_class("Matern52_1d"),
+          "Q": Q, "lr": 0.01, "llk_weight": 200.0, "freq_scale": 30.0, "logdet": True, "nepoch": nepoch,
+          "change_point": change_point, "tol": -1.0, "num_u_trick": 1, "other_paras": ""}
+    m = GP_solver_1d_extra(prob["xind"], prob["y"], prob["x"].reshape(-1, 1), prob["src"], 1e-6, Xte, Yte, tp)
+    return m, prob, (Xte, Yte)
+
+
+@pytest.mark.parametrize("eq", ["poisson", "allencahn"])
+def test_extra_gp_loss_grad(eq):
+    """Extra-GP second phase on the device (shifted data + Allen-Cahn offset) vs the oracle's
+    literal loss_extra (model_GP_solver_1d_extra.py:101-137), first GP frozen at random params."""
+    from tests.helpers import extra_params
+    m, prob, _ = _extra_model(eq, "Matern52_Cos_1d", 48, 5)
+    _, params, _ = problem_1d(eq=eq, kind="Matern52_Cos_1d", n=48, Q=5, seed=11)
+    prob_t = dict(prob, eq=eq)
+    try:
+        m._make_extra(params)
+        pe = extra_params(np.random.default_rng(12), 48)
+        loss, g = m.value_and_grad_extra(pe)
+        lo, go = O.loss_grad_1d_extra(prob_t, params, pe, "Matern52_1d")
+        c = max(np.linalg.cond(O.kernel_matrix("Matern52_Cos_1d", prob["x"], params["kernel_paras"], prob["jitter"])),
+                np.linalg.cond(O.kernel_matrix("Matern52_1d", prob["x"], O._extra_kp(pe["kernel_paras"]), prob["jitter"])))
+        tol = max(1e-9, 100 * c * np.finfo(float).eps)
+        assert abs(loss - lo) / abs(lo) < tol, (loss, lo)
+        for k in ("log_tau", "log_v"):
+            assert abs(g[k] - go[k]) <= tol * max(1.0, abs(go[k])), k
+        assert rel(g["u"], go["u"]) < tol
+        assert rel(g["kernel_paras"]["log-w"], go["kernel_paras"]["log-w"]) < tol
+        assert rel(g["kernel_paras"]["log-ls"], go["kernel_paras"]["log-ls"]) < tol
+        # criterion of both GPs together (compute_early_stopping_extra, :180-193)
+        assert abs(m.compute_early_stopping_extra(pe) - O.criterion_1d_extra(prob_t, params, pe, "Matern52_1d")) \
+            < tol * O.criterion_1d_extra(prob_t, params, pe, "Matern52_1d")
+    finally:
+        m.close()
+
+
+def test_extra_gp_two_phase_train_matches_replay():
+    """GP_solver_1d_extra.train (two phases, records incl. the change-point preds_extra quirk)
+    vs the oracle's replay of model_GP_solver_1d_extra.py:195-339, 40 epochs, N=64."""
+    m, prob, test = _extra_model("poisson", "Matern52_Cos_1d", 64, 6, nepoch=40)
+    try:
+        log, es, min_err = m.train(40, verbose=False)
+        _, pe, rec = O.train_replay_extra(prob, "Matern52_1d", 6, 30.0, 0.01, 40, 0.5, test)
+        assert log["epoch_list"] == rec["epoch_list"]
+        assert rel(log["loss_list"], rec["loss_list"]) < 1e-8
+        assert rel(log["err_list"], rec["err_list"]) < 1e-6
+        assert abs(min_err - rec["min_err"]) < 1e-6 * rec["min_err"]
+        assert rel(O.flatten_params(m.params_extra), O.flatten_params(pe)) < 1e-6
+    finally:
+        m.close()

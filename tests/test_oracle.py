@@ -70,6 +70,41 @@ def test_loss_grad_1d_vs_autograd(kind, eq):
     assert rel(O.flatten_params(go), O.flatten_params(ga)) < tol
 
 
+@pytest.mark.parametrize("kind_extra", ["Matern52_1d", "SE_1d"])
+@pytest.mark.parametrize("eq", ["poisson", "allencahn"])
+def test_loss_grad_1d_extra_vs_autograd(kind_extra, eq):
+    """The extra GP's loss (model_GP_solver_1d_extra.py:101-137): closed-form oracle vs the
+    literal torch transcription, first GP frozen at random params."""
+    from tests.helpers import extra_params
+    prob, params, _ = problem_1d(eq=eq, kind="Matern52_Cos_1d", n=30, Q=4, seed=3)
+    pe = extra_params(np.random.default_rng(5), 30)
+    lo, go = O.loss_grad_1d_extra(prob, params, pe, kind_extra)
+    la, ga = AR.loss_grad_1d_extra(prob, params, pe, kind_extra)
+    cond = max(np.linalg.cond(O.kernel_matrix("Matern52_Cos_1d", prob["x"], params["kernel_paras"], prob["jitter"])),
+               np.linalg.cond(O.kernel_matrix(kind_extra, prob["x"], O._extra_kp(pe["kernel_paras"]), prob["jitter"])))
+    tol = max(1e-11, 100 * cond * np.finfo(float).eps)
+    assert abs(lo - la) / abs(la) < tol
+    assert rel(O.flatten_params(go), O.flatten_params(ga)) < tol
+
+
+def test_extra_loss_is_shifted_1d_loss():
+    """The identity the device path relies on: loss_extra == the single-GP 1D loss of the extra
+    GP on (y - u[Xind], f - u_xx) for Poisson (gpk/model_GP_solver_1d_extra.py docstring)."""
+    from tests.helpers import extra_params
+    prob, params, _ = problem_1d(eq="poisson", kind="SE_Cos_1d", n=26, Q=3, seed=4)
+    pe = extra_params(np.random.default_rng(6), 26)
+    lo, go = O.loss_grad_1d_extra(prob, params, pe, "Matern52_1d")
+    u, uxx = O.frozen_fields_1d(prob, params)
+    shifted = dict(prob, kind="Matern52_1d", y=prob["y"] - u[prob["xind"]], src=prob["src"] - uxx)
+    ps = dict(pe, kernel_paras=O._extra_kp(pe["kernel_paras"]))
+    ls, gs = O.loss_grad_1d(shifted, ps)
+    assert abs(lo - ls) / abs(lo) < 1e-12
+    for k in ("log_tau", "log_v"):
+        assert abs(go[k] - gs[k]) <= 1e-9 * max(1.0, abs(go[k]))
+    assert rel(go["u"], gs["u"]) < 1e-10
+    assert rel(go["kernel_paras"]["log-w"], gs["kernel_paras"]["log-w"]) < 1e-10
+
+
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("eq", ["poisson", "allencahn", "advection"])
 def test_loss_grad_2d_vs_autograd(kind, eq):
