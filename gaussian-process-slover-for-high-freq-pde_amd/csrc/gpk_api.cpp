@@ -1205,6 +1205,18 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     *alg_flops = flops;
     *alg_bytes = bytes;
     return read_status(h);
+  } else if (nm == "spd_tiles" && h->bigspd) {
+    // the update launch's tile work alone (no pivot workgroup), sweep 0; idempotent enough for
+    // timing (each launch re-reads X and Z; values drift but stay finite over a few launches)
+    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
+    TRY(check_launch(launch_spd_big_stage(sa, L.naxes, -1, h->s), "pivot_init"));
+    TRY(check_launch(launch_spd_big_stage(sa, L.naxes, 0, h->s), "panel"));
+    launch = [&]() { return launch_spd_big_stage(sa, L.naxes, 1000001, h->s); };
+    for (int a = 0; a < L.naxes; ++a) {
+      const double n = a == 0 ? n1 : n2;
+      flops += n * n * n / spd_big_sweeps(a == 0 ? L.p1 : L.p2);
+      bytes += 8.0 * n * n;
+    }
   } else if ((nm == "spd_pivot" || nm == "spd_panel") && h->bigspd) {
     // large path pieces (idempotent): the 64-pivot factorisation of block 0, the panel of sweep 0
     TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));

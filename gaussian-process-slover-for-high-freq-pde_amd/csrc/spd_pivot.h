@@ -6,6 +6,7 @@
 namespace gpk {
 
 constexpr int SP = 33;  // pivot scratch stride
+typedef __attribute__((address_space(3))) double* lds_ptr;
 
 __device__ __forceinline__ double rsqrt_f64(double p) {
   double y = __builtin_amdgcn_rsq(p);          // ~2^-29 relative
@@ -31,9 +32,11 @@ __device__ __forceinline__ double rsqrt_f64(double p) {
 // suffices.  The 4x4 square roots use v_rsq_f64 + two Newton steps (no fp64 sqrt/div
 // sequences).  Measured 7.0 us vs 12.5 us for the unblocked one-column-per-barrier form
 // (tools/probes/pivot1w_probe.hip); results agree to 3e-13 relative (M K M^T = I to 3e-13).
-template <int BS = 4>
-__device__ __forceinline__ double pivot_chol_inv_block(double* A, double* M, double* pv, int t,
-                                                       int* status) {
+// LP: the LDS pointer type -- plain double* when inlined into a kernel (address space inferred),
+// lds_ptr (address_space(3)) when called through a non-inlined function, so that the callee
+// still issues ds_read / ds_write instead of flat memory instructions.
+template <int BS = 4, typename LP = double*>
+__device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t, int* status) {
   const int c = t & 31, i0 = t >> 5;
   double a[4], m[4];
 #pragma unroll
