@@ -14,8 +14,10 @@ DESIGN.md §Multi-GPU).  Timing: barrier + device sync on both sides of exactly 
 max over ranks; value = total steps of all ranks / that time.
 
 Also reported: the dominant kernel's roofline (HIP events on the library's stream, algorithmic
-bytes/flops per launch), fp64 SPD factor+inverse GFLOP/s, and the CPU
-oracle timed on this host on a bounded sample (rank 0, N = 1 only).
+bytes/flops per launch), fp64 SPD factor+inverse GFLOP/s, the CPU
+oracle timed on this host on a bounded sample (rank 0, N = 1 only), and `large_factors`: the
+MFMA-bound kernels at C5's 4096^2 size (GEMM TF/s and fraction of the fp64 peak, the large SPD
+inverse, C5 ms/step; rank 0, N = 1 only, --no-large to skip).
 """
 import argparse
 import json
@@ -88,6 +90,31 @@ def cpu_baseline(config, seconds, max_steps=400):
                       f"C fields on {threads} threads)"}
 
 
+def large_factors(steps=3):
+    """The MFMA-bound end of the path on C5's 4096^2 grid (BASELINE.json configs[4]): the
+    128x128-tile GEMM stage gemm_B (S = A K2^{-1} and the residual R = beta D1 A + Bt D2^T - F:
+    three 4096^3 products), the 64-wide SPD inverse of both 4096 factors (n^3 flops each =
+    potrf + potri) and whole steps.  Not the headline; shows fp64 MFMA utilisation at size."""
+    from gpk.problems import make_solver
+    s = make_solver("C5", seed=0)
+    try:
+        s.step(1)
+        t0 = time.perf_counter()
+        s.step(steps)
+        step_ms = (time.perf_counter() - t0) / steps * 1e3
+        us, fl, _ = s.bench_kernel("gemm_B", 5)
+        inv_us = s.time_spd_inverse(3)
+        n = 4096
+        tus, tfl, _ = s.bench_kernel("spd_tiles", 3)
+    finally:
+        s.close()
+    gemm_tf = fl / (us * 1e-6) / 1e12
+    return {"config": "C5: advection 4096x4096, Matern52_Cos_1d, Q=30, fp64", "step_ms": step_ms,
+            "gemm_B_us": us, "gemm_tflops": gemm_tf, "gemm_mfma_frac": gemm_tf / PEAK_F64_TFLOPS,
+            "spd_inverse_ms": inv_us / 1e3, "cholesky_gflops": 2 * n ** 3 / (inv_us * 1e-6) / 1e9,
+            "spd_update_tflops": tfl / (tus * 1e-6) / 1e12}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,6 +124,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=50)
+    ap.add_argument("--no-large", action="store_true", help="skip the C5-size MFMA section")
     a = ap.parse_args()
 
     from gpk import replicas
@@ -143,6 +171,13 @@ def main():
     roof["alg_flops_per_launch"] = d["flops"]
     roof["alg_bytes_per_launch"] = d["bytes"]
 
+    large = None
+    if rank == 0 and world == 1 and not a.no_large:
+        try:
+            large = large_factors()
+        except Exception as e:  # reported, never required
+            large = {"error": f"{type(e).__name__}: {e}"}
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
@@ -174,6 +209,7 @@ def main():
             "roofline": roof,
             "kernels_us": {k: round(v["us"], 3) for k, v in kern.items()},
             "cpu_baseline": cpu,
+            "large_factors": large,
             "final_loss": float(losses[-1]),
         }
         print(json.dumps(out), flush=True)
