@@ -115,6 +115,37 @@ def large_factors(steps=3):
             "spd_update_tflops": tfl / (tus * 1e-6) / 1e12}
 
 
+def main_sharded(a):
+    """One 2D problem (--config) row-sharded over all ranks (gpk/shard.py): every rank runs its
+    rows of every product, RCCL all-gathers / all-reduces inside the step graph.  value = steps
+    of the single problem per second (strong scaling)."""
+    from gpk import replicas, shard
+    from gpk.problems import CONFIGS
+    ctx = replicas.init("nccl")
+    cfg = CONFIGS[a.config]
+    s = shard.make_sharded_solver(a.config, ctx, seed=0)
+    s.step(a.warmup)
+    replicas.barrier(ctx)
+    t0 = time.perf_counter()
+    losses = s.step(a.steps)
+    t1 = time.perf_counter()
+    replicas.barrier(ctx)
+    dt = replicas.max_over_ranks(t1 - t0, ctx)
+    if ctx.rank == 0:
+        n = cfg["n"]
+        print(json.dumps({
+            "metric": METRIC, "value": a.steps / dt, "unit": "iters/s", "n_gpus": ctx.world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: reference grid/source/boundary, U ~ 0.1 N(0,1) (seed 0, same on every rank)",
+            "config": {"workload": f"{a.config}: one {n}x{n} 2D problem row-sharded over {ctx.world} GPU(s)",
+                       "grid": [n, n], "Q": 30, "kernel": cfg["kernel"], "equation": cfg["equation"],
+                       "parallelism": f"row-sharded x{ctx.world} (RCCL all-gather / all-reduce)"},
+            "roofline": None, "cpu_baseline": None, "final_loss": float(losses[-1])}), flush=True)
+    s.close()
+    replicas.shutdown(ctx)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -125,7 +156,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--no-large", action="store_true", help="skip the C5-size MFMA section")
+    ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas",
+                    help="replicas: one independent problem per GPU (weak scaling, the default); "
+                         "sharded: ONE 2D problem row-sharded over the GPUs with RCCL (strong scaling)")
     a = ap.parse_args()
+    if a.mode == "sharded":
+        return main_sharded(a)
 
     from gpk import replicas
     from gpk.problems import CONFIGS, make_solver

@@ -7,9 +7,16 @@
 // a hipGraph that holds every kernel of the step in stream order:
 //   prep -> assemble K,D -> SPD inverse (+logdet) -> GEMM stages A..E (2D) | GEMVs (1D)
 //   -> hyperparameter-gradient contraction -> deterministic reduction -> loss + Adam.
+// A row-sharded handle (gpk_create_sharded / gpk_group_create) runs the 2D step across ranks:
+// see "row-sharded multi-GPU step" below.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -66,6 +73,12 @@ struct Stage {
 
 }  // namespace
 
+struct ShardComm;  // collective backend of a row-sharded handle (RCCL, or an in-process group)
+struct ShardGather {
+  double* buf;
+  size_t chunk;     // doubles per rank (a block of rows), rank r's block at buf + r * chunk
+};
+
 struct gpk_handle {
   gpk_problem prob{};
   double freq_scale = 0.0;
@@ -109,6 +122,15 @@ struct gpk_handle {
   double* uoff = nullptr;            // 1D Allen-Cahn offset (gpk_problem.uoff), or null
   // predict scratch
   GemmDesc* pdescs = nullptr;
+
+  // row-sharded step: this rank computes rows [rank*h, (rank+1)*h) of every GEMM output
+  bool shard = false;
+  int rank = 0, nranks = 1;
+  int h1 = 0, h2 = 0;                 // row-block heights of the P1- and P2-row outputs
+  ShardComm* comm = nullptr;
+  std::vector<GemmDesc> sdescs;       // row slices of hdescs
+  Stage sst[kGemmStages];
+  std::vector<ShardGather> sgather[kGemmStages];
 
   hipGraphExec_t g_exec[2] = {nullptr, nullptr};  // [apply]
   hipEvent_t ev[kMaxStages + 1] = {};
@@ -253,7 +275,10 @@ static TailArgs make_tail(gpk_handle* h, int apply) {
   return T;
 }
 
+static int enqueue_step_shard(gpk_handle* h, int apply);
+
 static int enqueue_step(gpk_handle* h, int apply) {
+  if (h->shard) return enqueue_step_shard(h, apply);
   const Layout& L = h->L;
   if (h->profiling) (void)hipEventRecord(h->ev[0], h->s);
   mark(h, 0);  // "prep" is fused into the assembly launch (stage kept for the name table)
@@ -479,8 +504,235 @@ static int build_descs(gpk_handle* h) {
   return GPK_OK;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// row-sharded multi-GPU step (the reference has no multi-GPU path)
+//
+// Every rank holds the whole problem, assembles and inverts both Kronecker factors itself
+// (replicated: O(N^2 Q) + O(N^3) per factor), and computes rows [r*h, (r+1)*h) of every
+// product of the step -- the GEMM stages are ~26 N^3 of the ~28 N^3 flops (C5: 1.9 TFLOP).
+// A row slice of C = op(A) op(B) needs only the same rows of op(A); every operand a later
+// stage reads beyond its own rows (a B operand, or an A operand read transposed) is completed
+// by an in-place all-gather of its row blocks.  The kernel-parameter contraction runs over a
+// 1/P share of the pair tiles; its partials, the per-tile loss partials (||R||^2, <A,Bt>) and
+// nothing else are all-reduced (6Q+2 tile vectors); the loss and the small-parameter Adam are
+// then identical on every rank; Adam on U updates the rank's rows, which are all-gathered.
+// Collectives: RCCL in the handle's stream (captured into the step's hipGraph), or -- for tests
+// on one GPU -- an in-process group of handles, one host thread per rank.
+// ------------------------------------------------------------------------------------------
+struct ShardComm {
+  virtual ~ShardComm() {}
+  virtual int allgather(gpk_handle* h, double* buf, size_t chunk) = 0;  // in place
+  virtual int allreduce(gpk_handle* h, double* buf, size_t n) = 0;      // in place, sum
+  virtual bool capturable() const = 0;
+};
+
+namespace {
+
+struct RcclComm : ShardComm {
+  ncclComm_t c = nullptr;
+  ~RcclComm() override {
+    if (c) (void)ncclCommDestroy(c);
+  }
+  int allgather(gpk_handle* h, double* buf, size_t chunk) override {
+    ncclResult_t r = ncclAllGather(buf + (size_t)h->rank * chunk, buf, chunk, ncclDouble, c, h->s);
+    return r == ncclSuccess ? GPK_OK : fail(GPK_ERCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  }
+  int allreduce(gpk_handle* h, double* buf, size_t n) override {
+    ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c, h->s);
+    return r == ncclSuccess ? GPK_OK : fail(GPK_ERCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  }
+  bool capturable() const override { return true; }
+};
+
+// In-process group (one device, one host thread per rank): collectives meet at a host barrier;
+// rank 0 moves the blocks with device copies (and sums in rank order: deterministic).
+struct LocalGroup {
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  long gen = 0;
+  bool broken = false;
+  std::vector<double*> slot;
+  bool barrier() {  // false if another rank failed
+    std::unique_lock<std::mutex> lk(mu);
+    if (broken) return false;
+    const long g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g || broken; });
+    }
+    return !broken;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    broken = true;
+    cv.notify_all();
+  }
+};
+
+struct LocalComm : ShardComm {
+  std::shared_ptr<LocalGroup> g;
+  int allgather(gpk_handle* h, double* buf, size_t chunk) override {
+    HIPCHK(hipStreamSynchronize(h->s));
+    g->slot[h->rank] = buf;
+    if (!g->barrier()) return fail(GPK_EHIP, "rank group aborted");
+    int rc = GPK_OK;
+    if (h->rank == 0) {
+      for (int src = 0; src < g->n && rc == GPK_OK; ++src)
+        for (int dst = 0; dst < g->n; ++dst)
+          if (dst != src &&
+              hipMemcpyAsync(g->slot[dst] + (size_t)src * chunk, g->slot[src] + (size_t)src * chunk,
+                             chunk * sizeof(double), hipMemcpyDeviceToDevice, h->s) != hipSuccess)
+            rc = fail(GPK_EHIP, "group all-gather copy");
+      if (hipStreamSynchronize(h->s) != hipSuccess) rc = fail(GPK_EHIP, "group all-gather sync");
+    }
+    if (!g->barrier()) return fail(GPK_EHIP, "rank group aborted");
+    return rc;
+  }
+  int allreduce(gpk_handle* h, double* buf, size_t n) override {
+    HIPCHK(hipStreamSynchronize(h->s));
+    g->slot[h->rank] = buf;
+    if (!g->barrier()) return fail(GPK_EHIP, "rank group aborted");
+    int rc = GPK_OK;
+    if (h->rank == 0) {
+      for (int src = 1; src < g->n && rc == GPK_OK; ++src)
+        rc = check_launch(launch_add_into(g->slot[0], g->slot[src], n, h->s), "add_into");
+      for (int dst = 1; dst < g->n && rc == GPK_OK; ++dst)
+        if (hipMemcpyAsync(g->slot[dst], g->slot[0], n * sizeof(double), hipMemcpyDeviceToDevice, h->s) != hipSuccess)
+          rc = fail(GPK_EHIP, "group all-reduce copy");
+      if (hipStreamSynchronize(h->s) != hipSuccess) rc = fail(GPK_EHIP, "group all-reduce sync");
+    }
+    if (!g->barrier()) return fail(GPK_EHIP, "rank group aborted");
+    return rc;
+  }
+  bool capturable() const override { return false; }
+};
+
+int tile_rows(int variant) { return variant == GEMM_SMALL ? 16 : variant == GEMM_BIG ? 64 : variant == GEMM_HUGE ? 128 : 32; }
+int tile_cols_count(const GemmDesc& d, int variant) {
+  const int tc = tile_rows(variant);
+  return (d.N + tc - 1) / tc;
+}
+
+// rows [r0, r0 + rows) of C = op(A) op(B) [+ dual] with every row-indexed operand offset
+GemmDesc slice_rows(const GemmDesc& d, int r0, int rows, int variant) {
+  GemmDesc s = d;
+  s.M = rows;
+  s.A = d.ta ? d.A + r0 : d.A + (size_t)r0 * d.lda;
+  if (d.K2) s.A2 = d.ta2 ? d.A2 + r0 : d.A2 + (size_t)r0 * d.lda2;
+  s.C = d.C + (size_t)r0 * d.ldc;
+  if (d.C0) s.C0 = d.C0 + (size_t)r0 * d.ldc0;
+  if (d.F) s.F = d.F + (size_t)r0 * d.ldf;
+  if (d.U) s.U = d.U + (size_t)r0 * d.ldf;
+  if (d.Q1) s.Q1 = d.Q1 + (size_t)r0 * d.ldf;
+  if (d.Q2) s.Q2 = d.Q2 + (size_t)r0 * d.ldf;
+  const size_t toff = (size_t)(r0 / tile_rows(variant)) * tile_cols_count(d, variant);
+  if (d.red) s.red = d.red + toff;
+  if (d.red2) s.red2 = d.red2 + toff;
+  return s;
+}
+
+}  // namespace
+
+// Row slices of the step's GEMM stages for this rank, the variant per stage (its tile rows must
+// divide the slice height so that the per-tile loss partials land in the full-grid slots), and
+// the all-gathers after each stage: exactly the outputs a later stage reads beyond its rows.
+static int build_shard(gpk_handle* h) {
+  const Layout& L = h->L;
+  const int P1 = L.p1, P2 = L.p2;
+  h->h1 = P1 / h->nranks;
+  h->h2 = P2 / h->nranks;
+  const int force = gemm_force(h->prob.flags);
+  h->sdescs.clear();
+  for (int k = 0; k < kGemmStages; ++k) {
+    const GemmDesc* full = h->hdescs.data() + h->st[k].off;
+    const int n = h->st[k].n;
+    std::vector<GemmDesc> tmp;
+    auto rows_of = [&](const GemmDesc& d) { return d.M == P1 ? h->h1 : h->h2; };
+    for (int i = 0; i < n; ++i) {
+      const GemmDesc& d = full[i];
+      if (d.M != P1 && d.M != P2) return fail(GPK_EINVAL, "shard: unexpected GEMM row count");
+      const int rows = rows_of(d);
+      tmp.push_back(slice_rows(d, h->rank * rows, rows, GEMM_SMALL));
+    }
+    int variant = gemm_variant(tmp.data(), n, force);
+    for (int i = 0; i < n; ++i)
+      while (rows_of(full[i]) % tile_rows(variant) != 0) variant = variant == GEMM_HUGE ? GEMM_BIG : GEMM_SMALL;
+    h->sst[k].off = (int)h->sdescs.size();
+    h->sst[k].n = n;
+    h->sst[k].variant = variant;
+    for (int i = 0; i < n; ++i) {
+      const int rows = rows_of(full[i]);
+      h->sdescs.push_back(slice_rows(full[i], h->rank * rows, rows, variant));
+      if (full[i].red) h->nquad = h->negap = gemm_tiles(full[i], variant);
+    }
+  }
+  auto g1 = [&](double* b) { return ShardGather{b, (size_t)h->h1 * P2}; };
+  for (auto& v : h->sgather) v.clear();
+  h->sgather[0] = {g1(h->A)};                                  // A_res: K1 A
+  h->sgather[1] = {g1(h->W1)};                                 // A_fix: K1^{-1} W1
+  h->sgather[2] = {g1(h->A), g1(h->Bt)};                       // R: D1 A; G_D*, G_K*: A^T, Bt
+  h->sgather[3] = {g1(h->R)};                                  // T1 = D1^T R; G_D2 = R^T Bt
+  h->sgather[5] = {g1(h->S)};                                  // G_K2: S^T Bt
+  h->sgather[6] = {g1(h->T1), ShardGather{h->GD[0], (size_t)h->h1 * P1},  // X1 = K1^{-1} T1;
+                   ShardGather{h->GD[1], (size_t)h->h2 * P2}};            // pgrad reads G_D whole
+  h->sgather[7] = {g1(h->X1)};                                 // D_res: K1 X1
+  h->sgather[8] = {g1(h->W1)};                                 // D_fix: K1^{-1} W1
+  h->sgather[9] = {g1(h->X2)};                                 // G_K2: X2^T Bt
+  h->sgather[10] = {ShardGather{h->GK[0], (size_t)h->h1 * P1}, ShardGather{h->GK[1], (size_t)h->h2 * P2}};
+  return GPK_OK;
+}
+
+static int enqueue_step_shard(gpk_handle* h, int apply) {
+  const Layout& L = h->L;
+  TRY(enqueue_assemble_inverse(h, apply));  // replicated: K, D, K^{-1}, log det, step constants
+  for (int k = 0; k < kGemmStages; ++k) {
+    TRY(check_launch(launch_gemm_auto(h->sdescs.data() + h->sst[k].off, h->sst[k].n, h->sc, h->s,
+                                      h->sst[k].variant), "gemm"));
+    for (const ShardGather& g : h->sgather[k]) TRY(h->comm->allgather(h, g.buf, g.chunk));
+  }
+  PGradArgs pa[2];
+  for (int a = 0; a < 2; ++a) {
+    pa[a] = PGradArgs{};
+    pa[a].x = a == 0 ? h->x1 : h->x2;
+    pa[a].n = a == 0 ? L.n1 : L.n2;
+    pa[a].p = a == 0 ? L.p1 : L.p2;
+    pa[a].kc = h->kc + a;
+    pa[a].GK = h->GK[a];
+    pa[a].GD = h->GD[a];
+    pa[a].deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
+    pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
+  }
+  TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, nullptr, h->rank,
+                                h->nranks), "pgrad"));
+  TRY(check_launch(launch_reduce_parts(h->pgpart, h->bpa, 2, L.q, h->pg, h->s), "reduce_parts"));
+  TRY(h->comm->allreduce(h, h->pg, (size_t)2 * 3 * QMAX));
+  TRY(h->comm->allreduce(h, h->red_egap, (size_t)h->negap));
+  TRY(h->comm->allreduce(h, h->red_quad, (size_t)h->nquad));
+  TailArgs T = make_tail(h, apply);
+  TRY(check_launch(launch_finalize(T.fin, h->s), "finalize"));
+  // this rank's tile slots are rewritten next step; the summed copies must not leak into it
+  HIPCHK(hipMemsetAsync(h->red_egap, 0, (size_t)h->negap * sizeof(double), h->s));
+  HIPCHK(hipMemsetAsync(h->red_quad, 0, (size_t)h->nquad * sizeof(double), h->s));
+  AdamUArgs au = T.adam;
+  const int r0 = h->rank * h->h1, r1 = std::min(L.n1, r0 + h->h1);
+  const int nu = L.n1 * L.n2;
+  au.e0 = r0 < r1 ? r0 * L.n2 : nu;
+  au.e1 = r0 < r1 ? r1 * L.n2 : nu;
+  TRY(check_launch(launch_adam_u(au, h->s), "adam_u"));
+  TRY(h->comm->allgather(h, h->Up, (size_t)h->h1 * L.p2));
+  return GPK_OK;
+}
+
 static int capture(gpk_handle* h, int apply) {
   if (h->g_exec[apply]) return GPK_OK;
+  if (h->shard && !h->comm->capturable())
+    return fail(GPK_EINVAL, "handle belongs to an in-process rank group: use gpk_group_step / gpk_group_loss_grad");
   hipGraph_t g = nullptr;
   HIPCHK(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
   int rc = enqueue_step(h, apply);
@@ -579,7 +831,10 @@ int gpk_kernel_matrices(int32_t kind, int32_t deriv, const double* x1, int32_t n
   return GPK_OK;
 }
 
-static Layout make_layout(const gpk_problem* p) {
+// padm: padding multiple of the matrix dimensions (32; 32 * nranks for a row-sharded handle so
+// that every rank's row block is a whole number of 32-row tiles)
+static Layout make_layout(const gpk_problem* p, int padm = PADM) {
+  auto pad_up = [padm](int n) { return (n + padm - 1) / padm * padm; };
   Layout L{};
   L.dim = p->dim;
   L.q = p->q;
@@ -630,7 +885,8 @@ static std::vector<double> init_params(const gpk_problem* p, const Layout& L, do
   return h;
 }
 
-int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
+static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nranks, bool shard,
+                       gpk_handle** out) {
   if (!p || !out) return fail(GPK_EINVAL, "NULL argument");
   *out = nullptr;
   if (p->dim != 1 && p->dim != 2) return fail(GPK_EINVAL, "dim must be 1 or 2");
@@ -654,7 +910,10 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
   if (p->dim == 2) h->prob.nb = 2 * p->n1 + 2 * p->n2;
   h->freq_scale = freq_scale;
   h->dev = p->device;
-  h->L = make_layout(p);
+  h->shard = shard;
+  h->rank = rank;
+  h->nranks = nranks;
+  h->L = make_layout(p, shard ? PADM * nranks : PADM);
   h->hyper = AdamHyper{p->lr, p->b1, p->b2, p->eps};
   const Layout& L = h->L;
   {
@@ -756,7 +1015,139 @@ int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
     h->Kinv[a] = h->bigspd ? h->K[a] : ((T & 1) ? h->Kb[a] : h->K[a]);
   }
   if (L.dim == 2 && (rc = build_descs(h)) != GPK_OK) return bail(rc);
+  if (shard && (rc = build_shard(h)) != GPK_OK) return bail(rc);
   *out = h;
+  return GPK_OK;
+}
+
+int gpk_create(const gpk_problem* p, double freq_scale, gpk_handle** out) {
+  return create_impl(p, freq_scale, 0, 1, false, out);
+}
+
+int gpk_comm_unique_id(uint8_t* out, int32_t len) {
+  if (!out || len < (int32_t)sizeof(ncclUniqueId)) return fail(GPK_EINVAL, "need a 128-byte buffer");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return fail(GPK_ERCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(out, &id, sizeof(id));
+  return GPK_OK;
+}
+
+int gpk_create_sharded(const gpk_problem* p, double freq_scale, int32_t rank, int32_t nranks,
+                       const uint8_t* comm_id, gpk_handle** out) {
+  if (!p || !out || !comm_id) return fail(GPK_EINVAL, "NULL argument");
+  if (p->dim != 2) return fail(GPK_EINVAL, "row-sharded handles are 2D (Kronecker) only");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(GPK_EINVAL, "bad rank / nranks");
+  gpk_handle* h = nullptr;
+  TRY(create_impl(p, freq_scale, rank, nranks, true, &h));
+  DevSwitch ds(h->dev);
+  RcclComm* c = new RcclComm();
+  ncclUniqueId id;
+  std::memcpy(&id, comm_id, sizeof(id));
+  ncclResult_t r = ncclCommInitRank(&c->c, nranks, id, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    gpk_destroy(h);
+    return fail(GPK_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  h->comm = c;
+  *out = h;
+  return GPK_OK;
+}
+
+int gpk_group_create(const gpk_problem* p, double freq_scale, int32_t nranks, gpk_handle** out) {
+  if (!p || !out) return fail(GPK_EINVAL, "NULL argument");
+  if (p->dim != 2) return fail(GPK_EINVAL, "row-sharded handles are 2D (Kronecker) only");
+  if (nranks < 1 || nranks > 64) return fail(GPK_EINVAL, "nranks must be in [1, 64]");
+  auto g = std::make_shared<LocalGroup>();
+  g->n = nranks;
+  g->slot.assign(nranks, nullptr);
+  for (int r = 0; r < nranks; ++r) out[r] = nullptr;
+  for (int r = 0; r < nranks; ++r) {
+    int rc = create_impl(p, freq_scale, r, nranks, true, &out[r]);
+    if (rc != GPK_OK) {
+      for (int k = 0; k < r; ++k) gpk_destroy(out[k]);
+      return rc;
+    }
+    LocalComm* c = new LocalComm();
+    c->g = g;
+    out[r]->comm = c;
+  }
+  return GPK_OK;
+}
+
+// one host thread per rank, eager launches (an in-process group cannot be graph-captured)
+static int group_run(gpk_handle** hs, int nranks, int apply, int n_steps) {
+  if (!hs || nranks < 1) return fail(GPK_EINVAL, "bad group");
+  for (int r = 0; r < nranks; ++r)
+    if (!hs[r] || !hs[r]->shard || hs[r]->comm->capturable() || hs[r]->rank != r || hs[r]->nranks != nranks)
+      return fail(GPK_EINVAL, "not the handles of one gpk_group_create group, in rank order");
+  std::vector<int> rcs(nranks, GPK_OK);
+  std::vector<std::string> errs(nranks);
+  std::vector<std::thread> th;
+  for (int r = 0; r < nranks; ++r)
+    th.emplace_back([&, r]() {
+      gpk_handle* h = hs[r];
+      DevSwitch ds(h->dev);
+      int rc = hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s) == hipSuccess ? GPK_OK : GPK_EHIP;
+      for (int i = 0; i < n_steps && rc == GPK_OK; ++i) rc = enqueue_step_shard(h, apply);
+      if (rc == GPK_OK && hipStreamSynchronize(h->s) != hipSuccess) rc = fail(GPK_EHIP, "group step sync");
+      if (rc != GPK_OK) {
+        errs[r] = g_err;
+        static_cast<LocalComm*>(h->comm)->g->abort();
+      }
+      rcs[r] = rc;
+    });
+  for (auto& t : th) t.join();
+  for (int r = 0; r < nranks; ++r)
+    if (rcs[r] != GPK_OK) return fail(rcs[r], "rank " + std::to_string(r) + ": " + errs[r]);
+  int rc = GPK_OK;
+  for (int r = 0; r < nranks && rc == GPK_OK; ++r) {
+    DevSwitch ds(hs[r]->dev);
+    rc = read_status(hs[r]);
+  }
+  return rc;
+}
+
+int gpk_group_step(gpk_handle** hs, int32_t nranks, int32_t n_steps, double* losses) {
+  if (n_steps < 0 || n_steps > LOSS_CAP) return fail(GPK_EINVAL, "n_steps must be in [0, 4096]");
+  TRY(group_run(hs, nranks, 1, n_steps));
+  if (losses && n_steps > 0) {
+    DevSwitch ds(hs[0]->dev);
+    HIPCHK(hipMemcpy(losses, hs[0]->losses, n_steps * sizeof(double), hipMemcpyDeviceToHost));
+  }
+  return GPK_OK;
+}
+
+int gpk_group_loss_grad(gpk_handle** hs, int32_t nranks, double* loss, double* grad_flat) {
+  if (!loss) return fail(GPK_EINVAL, "NULL argument");
+  TRY(group_run(hs, nranks, 0, 1));
+  const Layout& L = hs[0]->L;
+  DevSwitch ds(hs[0]->dev);
+  HIPCHK(hipMemcpy(loss, hs[0]->diag, sizeof(double), hipMemcpyDeviceToHost));
+  if (grad_flat) {  // small params from rank 0 (identical on every rank), U rows from their owner
+    HIPCHK(hipMemcpy(grad_flat, hs[0]->grad, L.nparams * sizeof(double), hipMemcpyDeviceToHost));
+    for (int r = 1; r < nranks; ++r) {
+      const int r0 = r * hs[r]->h1, r1 = std::min(L.n1, r0 + hs[r]->h1);
+      if (r0 >= r1) continue;
+      HIPCHK(hipMemcpy(grad_flat + L.off_u + (size_t)r0 * L.n2, hs[r]->grad + L.off_u + (size_t)r0 * L.n2,
+                       (size_t)(r1 - r0) * L.n2 * sizeof(double), hipMemcpyDeviceToHost));
+    }
+  }
+  return GPK_OK;
+}
+
+int gpk_shard_info(const gpk_handle* h, int32_t* rank, int32_t* nranks, int32_t* row0, int32_t* rows) {
+  if (!h || !rank || !nranks || !row0 || !rows) return fail(GPK_EINVAL, "NULL argument");
+  *rank = h->rank;
+  *nranks = h->nranks;
+  if (!h->shard) {
+    *row0 = 0;
+    *rows = h->L.n1;
+    return GPK_OK;
+  }
+  *row0 = h->rank * h->h1;
+  *rows = std::max(0, std::min(h->L.n1, *row0 + h->h1) - *row0);
   return GPK_OK;
 }
 
@@ -770,6 +1161,7 @@ int gpk_destroy(gpk_handle* h) {
     if (h->ev[k]) (void)hipEventDestroy(h->ev[k]);
   for (void* p : h->allocs) (void)hipFree(p);
   if (h->s) (void)hipStreamDestroy(h->s);
+  delete h->comm;
   delete h;
   return GPK_OK;
 }
@@ -794,6 +1186,8 @@ int gpk_get_params(gpk_handle* h, double* flat, int64_t n) {
   if (!h || !flat) return fail(GPK_EINVAL, "NULL argument");
   if (n != h->L.nparams) return fail(GPK_EINVAL, "parameter count mismatch");
   DevSwitch ds(h->dev);
+  if (h->shard)  // U rows are gathered into Up each step; the flat params hold only this rank's
+    TRY(check_launch(launch_params_from_up(h->Up, h->L, h->params, h->s), "params_from_up"));
   HIPCHK(hipMemcpyAsync(flat, h->params, n * sizeof(double), hipMemcpyDeviceToHost, h->s));
   HIPCHK(hipStreamSynchronize(h->s));
   return GPK_OK;

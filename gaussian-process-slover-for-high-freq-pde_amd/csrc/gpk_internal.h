@@ -241,7 +241,7 @@ struct TailArgs;  // stepk.h
 // tail (nullable): the fused step tail carried by the same launch (stepk.h TailArgs)
 hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int naxes,
                         int blocks_per_axis, const StepScalars* sc, hipStream_t s,
-                        const TailArgs* tail = nullptr);
+                        const TailArgs* tail = nullptr, int shard_rank = 0, int shard_n = 1);
 int pgrad_blocks(int n);
 
 }  // namespace gpk

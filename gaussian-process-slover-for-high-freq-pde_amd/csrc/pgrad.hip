@@ -31,6 +31,7 @@ struct PGradBatch {
   PGradArgs ax[2];
   int tiles[2];
   int naxes, bpa;
+  int shard_rank, shard_n;  // row-sharded step: this rank contracts pair tiles t % shard_n == rank
   TailArgs tail;
 };
 
@@ -120,6 +121,9 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
     if (b.tail.fused) pgrad_tail(b, axis, blk, q);
     return;
   }
+  // sharded step (never fused): another rank's pair tile -- this slot is never written, so it
+  // stays zero and the cross-rank all-reduce of the reduced partials counts each tile once
+  if (b.shard_n > 1 && tile % b.shard_n != b.shard_rank) return;
   int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
   while ((I + 1) * (I + 2) / 2 <= tile) ++I;
   while (I * (I + 1) / 2 > tile) --I;
@@ -254,8 +258,11 @@ static void launch_pg_t(const PGradBatch& b, int naxes, int bpa, int q, int deri
 
 hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int naxes,
                         int blocks_per_axis, const StepScalars* sc, hipStream_t s,
-                        const TailArgs* tail) {
+                        const TailArgs* tail, int shard_rank, int shard_n) {
   PGradBatch b{};
+  b.shard_rank = shard_rank;
+  b.shard_n = shard_n;
+  if (shard_n > 1 && tail && tail->fused) return hipErrorInvalidValue;
   for (int k = 0; k < naxes; ++k) {
     b.ax[k] = a[k];
     int T = a[k].p / 32;

@@ -49,6 +49,7 @@ struct AdamUArgs {
   const double* S; const double* X1; const double* X2; const double* R;
   double* Up;
   const double* U0;  // 1D Allen-Cahn offset (extra-GP second phase), nullable
+  int e0, e1;        // element range [e0, e1) of the solution grid (row-sharded step); e1 = 0: all
   const double* bvals;
   const int* bidx; int nb;
   double* params; double* grad; double* m; double* v;
@@ -76,5 +77,7 @@ hipError_t launch_reduce_parts(const double* part, int bpa, int naxes, int q, do
 hipError_t launch_finalize(const FinalizeArgs& f, hipStream_t s);
 hipError_t launch_adam_u(const AdamUArgs& a, hipStream_t s);
 hipError_t launch_sync_u(const double* params, const Layout& L, double* Up, hipStream_t s);
+hipError_t launch_params_from_up(const double* Up, const Layout& L, double* params, hipStream_t s);
+hipError_t launch_add_into(double* dst, const double* src, size_t n, hipStream_t s);
 
 }  // namespace gpk

@@ -73,6 +73,7 @@ hipError_t launch_finalize(const FinalizeArgs& f, hipStream_t s) {
 
 __global__ __launch_bounds__(256) void adam_u_kernel(AdamUArgs A) {
   const int e = blockIdx.x * 256 + threadIdx.x;
+  if (A.e1 > 0 && (e < A.e0 || e >= A.e1)) return;  // another rank's rows
   if (e < tail_nu(A.L)) adam_u_elem(A, e);
 }
 
@@ -96,6 +97,37 @@ __global__ void sync_u_kernel(const double* __restrict__ params, Layout L, doubl
 hipError_t launch_sync_u(const double* params, const Layout& L, double* Up, hipStream_t s) {
   const int nu = (L.dim == 2) ? L.n1 * L.n2 : L.n1;
   hipLaunchKernelGGL(sync_u_kernel, dim3((nu + 255) / 256), dim3(256), 0, s, params, L, Up);
+  return hipGetLastError();
+}
+
+}  // namespace gpk
+
+namespace gpk {
+
+// padded working copy of U -> flat params (row-sharded handles gather U rows into Up every step;
+// the flat params are refreshed from it before they are read back)
+__global__ void params_from_up_kernel(const double* __restrict__ Up, Layout L, double* params) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int nu = L.n1 * L.n2;
+  if (e >= nu) return;
+  params[L.off_u + e] = Up[(size_t)(e / L.n2) * L.p2 + e % L.n2];
+}
+
+hipError_t launch_params_from_up(const double* Up, const Layout& L, double* params, hipStream_t s) {
+  const int nu = L.n1 * L.n2;
+  hipLaunchKernelGGL(params_from_up_kernel, dim3((nu + 255) / 256), dim3(256), 0, s, Up, L, params);
+  return hipGetLastError();
+}
+
+// dst[i] += src[i]  (the in-process all-reduce of a local rank group)
+__global__ void add_into_kernel(double* __restrict__ dst, const double* __restrict__ src, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] += src[i];
+}
+
+hipError_t launch_add_into(double* dst, const double* src, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(add_into_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dst, src, n);
   return hipGetLastError();
 }
 

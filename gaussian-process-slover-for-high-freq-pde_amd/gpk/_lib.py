@@ -75,6 +75,14 @@ EXPORTS = {
     "gpk_kernel_pairs": ([ctypes.c_int32, ctypes.c_int32, _dp, _dp, ctypes.c_int64, _dp, _dp, _dp,
                           ctypes.c_int32, _dp], ctypes.c_int),
     "gpk_forward_field": ([ctypes.c_void_p, ctypes.c_int32, _dp, ctypes.c_int64], ctypes.c_int),
+    "gpk_comm_unique_id": ([ctypes.POINTER(ctypes.c_uint8), ctypes.c_int32], ctypes.c_int),
+    "gpk_create_sharded": ([ctypes.POINTER(gpk_problem), ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                            ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "gpk_group_create": ([ctypes.POINTER(gpk_problem), ctypes.c_double, ctypes.c_int32,
+                          ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "gpk_group_step": ([ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_int32, _dp], ctypes.c_int),
+    "gpk_group_loss_grad": ([ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, _dp, _dp], ctypes.c_int),
+    "gpk_shard_info": ([ctypes.c_void_p, _ip, _ip, _ip, _ip], ctypes.c_int),
 }
 
 _LIB = None

@@ -51,7 +51,7 @@ def params_template(dim, n1, n2, Q):
 class DeviceSolver:
     def __init__(self, dim, eq, kind, x1, src, bvals, x2=None, bidx=None, Q=30, jitter=1e-6,
                  llk_weight=200.0, logdet=True, beta=1.0, lr=0.01, freq_scale=20.0, device=0,
-                 b1=0.9, b2=0.999, eps=1e-8, flags=0, uoff=None):
+                 b1=0.9, b2=0.999, eps=1e-8, flags=0, uoff=None, shard=None):
         lib = _lib.load()
         self.dim = int(dim)
         self.eq = eq
@@ -93,13 +93,29 @@ class DeviceSolver:
                 raise ValueError("uoff must have n1 entries")
             p.uoff = dptr(self._uoff)
         self._prob = p
-        h = ctypes.c_void_p()
-        check(lib.gpk_create(ctypes.byref(p), float(freq_scale), ctypes.byref(h)))
-        self._h = h
+        self._h = self._create(lib, p, float(freq_scale), shard)
+        h = self._h
         n = ctypes.c_int64()
         check(lib.gpk_num_params(h, ctypes.byref(n)))
         self.nparams = n.value
         self.template = params_template(self.dim, self.n1, self.n2, self.Q)
+
+    def _create(self, lib, p, freq_scale, shard):
+        h = ctypes.c_void_p()
+        if shard is None:
+            check(lib.gpk_create(ctypes.byref(p), freq_scale, ctypes.byref(h)))
+        else:  # (rank, nranks, 128-byte RCCL id): one rank of a row-sharded group
+            rank, nranks, cid = shard
+            buf = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(cid))
+            check(lib.gpk_create_sharded(ctypes.byref(p), freq_scale, int(rank), int(nranks), buf,
+                                         ctypes.byref(h)))
+        return h
+
+    def shard_info(self):
+        """(rank, nranks, row0, rows): the rows of U this handle owns (all rows unsharded)."""
+        v = [ctypes.c_int32() for _ in range(4)]
+        check(_lib.load().gpk_shard_info(self._h, *[ctypes.byref(x) for x in v]))
+        return tuple(int(x.value) for x in v)
 
     # -- lifecycle ---------------------------------------------------------------------
     def close(self):
@@ -232,3 +248,61 @@ def kernel_matrices(kind, x1, x2, paras, jitter=0.0, deriv=0):
                                   dptr(ll), dptr(fr), lw.size, float(jitter), dptr(K),
                                   dptr(D) if deriv else None))
     return K, D
+
+
+def comm_unique_id():
+    """128-byte RCCL id for gpk_create_sharded (rank 0 makes it, every rank uses the same)."""
+    buf = (ctypes.c_uint8 * 128)()
+    check(_lib.load().gpk_comm_unique_id(buf, 128))
+    return bytes(buf)
+
+
+class DeviceGroup(DeviceSolver):
+    """`nranks` row-sharded handles of one 2D problem on ONE GPU, exchanging through device copies
+    (gpk_group_create): the multi-GPU sharded step with an in-process stand-in for RCCL, for
+    parity tests on a single device.  Same interface as DeviceSolver; set_* go to every rank,
+    loss_grad returns the full gradient (U rows collected from their owners)."""
+
+    def __init__(self, nranks, *args, **kw):
+        self.nranks = int(nranks)
+        super().__init__(*args, **kw)
+
+    def _create(self, lib, p, freq_scale, shard):
+        arr = (ctypes.c_void_p * self.nranks)()
+        check(lib.gpk_group_create(ctypes.byref(p), freq_scale, self.nranks, arr))
+        self._hs = arr
+        return ctypes.c_void_p(arr[0])
+
+    def close(self):
+        if getattr(self, "_hs", None) is not None:
+            lib = _lib.load()
+            for k in range(self.nranks):
+                if self._hs[k]:
+                    lib.gpk_destroy(self._hs[k])
+            self._hs = None
+            self._h = None
+
+    def set_flat(self, flat):
+        flat = f64(flat).reshape(-1)
+        for k in range(self.nranks):
+            check(_lib.load().gpk_set_params(self._hs[k], dptr(flat), flat.size))
+
+    def set_opt_state(self, count, mu, nu):
+        mu, nu = f64(mu).reshape(-1), f64(nu).reshape(-1)
+        for k in range(self.nranks):
+            check(_lib.load().gpk_set_opt_state(self._hs[k], int(count), dptr(mu), dptr(nu), self.nparams))
+
+    def loss_grad(self):
+        loss = ctypes.c_double()
+        g = np.empty(self.nparams)
+        check(_lib.load().gpk_group_loss_grad(self._hs, self.nranks, ctypes.byref(loss), dptr(g)))
+        return loss.value, g
+
+    def step(self, n=1, losses=True):
+        out = np.empty(max(int(n), 1))
+        done = 0
+        while done < n:
+            k = min(4096, n - done)
+            check(_lib.load().gpk_group_step(self._hs, self.nranks, k, dptr(out[done:])))
+            done += k
+        return out[:n] if losses else None

@@ -166,6 +166,30 @@ int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us);
 int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg_us,
                      double* alg_flops, double* alg_bytes);
 
+/* ---- Row-sharded 2D step across GPUs (the reference has no multi-GPU path).
+ * Every rank holds the problem, forms both Kronecker factors' K, D, K^{-1} itself, and computes
+ * its block of rows of every product of the step (model_GP_solver_2d.py:87-183 /
+ * advection :87-179); operands read beyond a rank's rows are completed by in-place all-gathers,
+ * the kernel-parameter partials and per-tile loss partials by all-reduces.  Loss, gradients of
+ * the small params and their Adam update are identical on every rank; Adam on U updates the
+ * rank's rows (gathered after the step).  gpk_step / gpk_loss_grad run this step on a sharded
+ * handle; gpk_loss_grad's U gradient is valid on the rank's rows only (gpk_shard_info). */
+
+/* 128-byte RCCL communicator id: rank 0 creates it, every rank passes the same bytes. */
+int gpk_comm_unique_id(uint8_t* out, int32_t len);
+/* One rank (one process, device = problem.device) of an RCCL (xGMI) group of nranks. */
+int gpk_create_sharded(const gpk_problem* p, double freq_scale, int32_t rank, int32_t nranks,
+                       const uint8_t* comm_id, gpk_handle** out);
+/* nranks handles on ONE device in this process, exchanging through device copies (the same
+ * sharded step without RCCL: tests on a single GPU).  Driven by gpk_group_step /
+ * gpk_group_loss_grad (one host thread per rank); gpk_step on them returns GPK_EINVAL. */
+int gpk_group_create(const gpk_problem* p, double freq_scale, int32_t nranks, gpk_handle** out);
+int gpk_group_step(gpk_handle** hs, int32_t nranks, int32_t n_steps, double* losses);
+/* loss and the FULL flat gradient (U rows collected from their owners) */
+int gpk_group_loss_grad(gpk_handle** hs, int32_t nranks, double* loss, double* grad_flat);
+/* this handle's rank, group size and rows [row0, row0 + rows) of U it owns */
+int gpk_shard_info(const gpk_handle* h, int32_t* rank, int32_t* nranks, int32_t* row0, int32_t* rows);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,137 @@
+"""Row-sharded 2D step (gpk_create_sharded / gpk_group_create).
+
+GPU: an in-process group of nranks handles on one device runs the same sharded step as RCCL
+ranks (only the collective transport differs); its loss / full gradient must match the CPU
+oracle and the unsharded handle, and its Adam trajectory the unsharded one.  RCCL itself is
+exercised with one rank (a one-GPU box cannot host two RCCL ranks).
+CPU: the communicator-id exchange over a world-size-2 gloo group.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import gp_oracle as O
+from tests.helpers import device_solver, problem_2d, rel
+
+
+def _group(prob, Q, fs, nranks, flags=0):
+    from gpk.core import DeviceGroup
+    return DeviceGroup(nranks, 2, prob["eq"], prob["kind"], prob["x1"], prob["src"], prob["bvals"],
+                       x2=prob["x2"], Q=Q, jitter=prob["jitter"], llk_weight=prob["llk_weight"],
+                       logdet=prob["logdet"], beta=prob.get("beta", 1.0), lr=0.01, freq_scale=fs,
+                       flags=flags)
+
+
+def _tol(prob, params):
+    c = max(np.linalg.cond(O.kernel_matrix(prob["kind"], prob["x1"], params["kernel_paras_1"], prob["jitter"])),
+            np.linalg.cond(O.kernel_matrix(prob["kind"], prob["x2"], params["kernel_paras_2"], prob["jitter"])))
+    return max(1e-10, 50 * c * np.finfo(float).eps)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks", [1, 2, 3, 4])
+@pytest.mark.parametrize("eq,kind,n1,n2", [("poisson", "Matern52_Cos_1d", 72, 56),
+                                          ("allencahn", "SE_Cos_1d", 40, 66),
+                                          ("advection", "Matern52_1d", 50, 90)])
+def test_group_loss_grad(eq, kind, n1, n2, nranks):
+    """Loss and full gradient of the sharded step vs the oracle and vs one unsharded handle
+    (unequal axes, ragged last row blocks, padding to 32 * nranks)."""
+    prob, params, _, fs = problem_2d(eq=eq, kind=kind, n1=n1, n2=n2, Q=5, seed=21)
+    g = _group(prob, 5, fs, nranks)
+    s = device_solver(prob, 5, fs)
+    try:
+        g.set_params(params)
+        s.set_params(params)
+        lg, gg = g.loss_grad()
+        ls, gs = s.loss_grad()
+        lo, go = O.loss_grad_2d(prob, params)
+        tol = _tol(prob, params)
+        assert abs(lg - lo) / abs(lo) < tol, (lg, lo)
+        assert rel(gg, O.flatten_params(go)) < tol
+        assert abs(lg - ls) / abs(ls) < 1e-11
+        assert rel(gg, gs) < 1e-9
+    finally:
+        g.close()
+        s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks,flags", [(2, 0), (4, 0), (2, 8)])
+def test_group_trajectory_matches_unsharded(nranks, flags):
+    """10 Adam steps of the sharded group == 10 steps of one handle (params, losses); flags 8
+    forces the 128x128 GEMM where the row blocks allow it (downgraded per stage otherwise)."""
+    prob, params, (Xte, _), fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=200, n2=136, Q=6, seed=3)
+    g = _group(prob, 6, fs, nranks, flags=flags)
+    s = device_solver(prob, 6, fs)
+    try:
+        g.set_params(params)
+        s.set_params(params)
+        lg = g.step(10)
+        ls = s.step(10)
+        assert rel(lg, ls) < 1e-11
+        assert rel(g.get_flat(), s.get_flat()) < 1e-9
+        assert rel(g.predict(Xte[0], Xte[1]), s.predict(Xte[0], Xte[1])) < 1e-9
+    finally:
+        g.close()
+        s.close()
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_sharded_handle():
+    """gpk_create_sharded with a one-rank RCCL communicator: the captured step with RCCL
+    all-gathers / all-reduces in its graph equals the unsharded step."""
+    from gpk.core import DeviceSolver, comm_unique_id
+    prob, params, _, fs = problem_2d(eq="poisson", kind="SE_Cos_1d", n1=64, n2=48, Q=4, seed=5)
+    kw = dict(x2=prob["x2"], Q=4, jitter=prob["jitter"], llk_weight=prob["llk_weight"],
+              logdet=prob["logdet"], lr=0.01, freq_scale=fs)
+    r = DeviceSolver(2, prob["eq"], prob["kind"], prob["x1"], prob["src"], prob["bvals"],
+                     shard=(0, 1, comm_unique_id()), **kw)
+    s = device_solver(prob, 4, fs)
+    try:
+        assert r.shard_info() == (0, 1, 0, 64)
+        r.set_params(params)
+        s.set_params(params)
+        lr_, gr = r.loss_grad()
+        ls, gs = s.loss_grad()
+        assert abs(lr_ - ls) / abs(ls) < 1e-12
+        assert rel(gr, gs) < 1e-10
+        assert rel(r.step(5), s.step(5)) < 1e-11
+        assert rel(r.get_flat(), s.get_flat()) < 1e-10
+    finally:
+        r.close()
+        s.close()
+
+
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from gpk import replicas, shard
+    ctx = replicas.init("gloo")
+    cid = shard.broadcast_comm_id(ctx, make_id=lambda: bytes((7 * i + 3) % 256 for i in range(128)))
+    q.put((rank, cid))
+    replicas.shutdown(ctx)
+
+
+def test_comm_id_broadcast_gloo_world2():
+    """Every rank of a 2-process gloo group receives rank 0's 128-byte communicator id."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = bytes((7 * i + 3) % 256 for i in range(128))
+    assert got[0] == expect and got[1] == expect
