@@ -1605,7 +1605,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
     TRY(check_launch(launch_spd_big_stage(sa, L.naxes, -1, h->s), "pivot_init"));
     TRY(check_launch(launch_spd_big_stage(sa, L.naxes, 0, h->s), "panel"));
-    launch = [&]() { return launch_spd_big_stage(sa, L.naxes, 1000001, h->s); };
+    launch = [&]() { return launch_spd_big_tiles(sa, L.naxes, 0, h->s); };
     for (int a = 0; a < L.naxes; ++a) {
       const double n = a == 0 ? n1 : n2;
       flops += n * n * n / spd_big_sweeps(a == 0 ? L.p1 : L.p2);

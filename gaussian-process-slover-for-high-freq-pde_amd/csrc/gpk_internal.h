@@ -150,6 +150,7 @@ constexpr int SPD_BIG_MIN = 1600;
 hipError_t launch_spd_inverse_big(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
 // stage -1: pivot 0; 2k: panel of sweep k; 2k+1: update of sweep k
 hipError_t launch_spd_big_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
+hipError_t launch_spd_big_tiles(SpdArgs* args, int nmat, int k, hipStream_t s);  // bench only
 int spd_big_sweeps(int p);
 
 // Iterative-refinement gate: a refinement GEMM/GEMV runs only when the factor's condition
