@@ -5,8 +5,10 @@ OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
 TAG=${1:-r1}
-timeout -k 10 600 python -m pytest tests -q -m gpu > $OUT/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> $OUT/pytest_gpu.log
+timeout -k 10 600 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc" >> $OUT/pytest_gpu.log
 tail -3 $OUT/pytest_gpu.log
+# rc 1 = ordinary test failures; anything else (abort, segfault, time limit) ends the call here
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest aborted rc=$rc"; tail -40 $OUT/pytest_gpu.log; exit 1; fi
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; cat $OUT/smoke.log; exit 1; }
 cat $OUT/smoke.log
 timeout -k 10 300 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { echo bench failed; tail -20 $OUT/bench_$TAG.err; exit 1; }
