@@ -155,6 +155,9 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
   const bool pivot_wg = (int)blockIdx.x == b.pivot_x;
   const int tile = blockIdx.x / ASM_SUB, sub = blockIdx.x % ASM_SUB;
   if (!pivot_wg && tile >= b.tiles[axis]) return;
+  // tile (0,0) feeds the pivot-0 workgroup, the critical path of the launch: its waves get
+  // issue priority over the other ~4 waves sharing each SIMD
+  if (b.pivot_x >= 0 && (tile == 0 || pivot_wg)) __builtin_amdgcn_s_setprio(3);
 
   __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
   __shared__ double pk[4][64], pd[4][64];

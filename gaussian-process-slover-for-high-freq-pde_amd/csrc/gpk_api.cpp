@@ -69,6 +69,7 @@ struct DevSwitch {  // restore the caller's current device on scope exit
 
 struct Stage {
   int off = 0, n = 0, variant = 0;
+  bool gated = false;  // every descriptor is a refinement GEMM (left out of the fast graph)
 };
 
 }  // namespace
@@ -132,7 +133,14 @@ struct gpk_handle {
   Stage sst[kGemmStages];
   std::vector<ShardGather> sgather[kGemmStages];
 
-  hipGraphExec_t g_exec[2] = {nullptr, nullptr};  // [apply]
+  hipGraphExec_t g_exec[2] = {nullptr, nullptr};  // [apply] full step graph
+  hipGraphExec_t g_fast[2] = {nullptr, nullptr};  // [apply] without the refinement stages
+  bool fast_ok = false;    // the fast graph exists for this handle (not row-sharded)
+  int fast_mode = 0;       // next step(s) run the fast graph (gate closed with margin last time)
+  long long rollbacks = 0;
+  double* snap = nullptr;  // [3 * nparams] params, m, v at the start of a fast batch
+  int* snap_count = nullptr;
+  unsigned int* viol = nullptr;  // the fast graph met an open refinement gate
   hipEvent_t ev[kMaxStages + 1] = {};
   bool profiling = false;
   int nstage = 0;
@@ -249,7 +257,7 @@ static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
 }
 
 // the step tail (loss, small-parameter Adam, dL/dU + Adam on U) fused into the pgrad launch
-static TailArgs make_tail(gpk_handle* h, int apply) {
+static TailArgs make_tail(gpk_handle* h, int apply, bool refine = true) {
   const Layout& L = h->L;
   const int ac = h->prob.eq == GPK_ALLENCAHN;
   TailArgs T{};
@@ -264,6 +272,10 @@ static TailArgs make_tail(gpk_handle* h, int apply) {
   f.params = h->params; f.grad = h->grad; f.m = h->m; f.v = h->v;
   f.losses = h->losses; f.loss_slot = h->loss_slot; f.diag = h->diag;
   f.bgap = h->bgap;
+  if (!refine) {  // fast graph: check that no refinement was needed
+    for (int a = 0; a < L.naxes; ++a) f.watch[a] = h->pst[a];
+    f.viol = h->viol;
+  }
   AdamUArgs& au = T.adam;
   au.L = L; au.hyper = h->hyper; au.llk_weight = h->prob.llk_weight; au.apply = apply; au.ac = ac;
   au.sc = h->sc; au.Up = h->Up; au.bvals = h->bvals; au.bidx = h->bidx; au.nb = h->prob.nb;
@@ -277,7 +289,7 @@ static TailArgs make_tail(gpk_handle* h, int apply) {
 
 static int enqueue_step_shard(gpk_handle* h, int apply);
 
-static int enqueue_step(gpk_handle* h, int apply) {
+static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
   if (h->shard) return enqueue_step_shard(h, apply);
   const Layout& L = h->L;
   if (h->profiling) (void)hipEventRecord(h->ev[0], h->s);
@@ -287,6 +299,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
   const int ac = h->prob.eq == GPK_ALLENCAHN;
   if (L.dim == 2) {
     for (int k = 0; k < kGemmStages; ++k) {
+      if (!refine && h->st[k].gated) continue;
       TRY(check_launch(launch_gemm_auto(h->hdescs.data() + h->st[k].off, h->st[k].n, h->sc, h->s,
                                         h->st[k].variant), "gemm"));
       mark(h, stage++);
@@ -303,7 +316,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
       pa[a].deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
     }
-    TailArgs tail = make_tail(h, apply);
+    TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, &tail), "pgrad"));
     mark(h, stage++);
   } else {
@@ -314,6 +327,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
     g.lda = P; g.p = P; g.rows = P; g.alpha = 1.0; g.ac = ac; g.F = h->F; g.U = h->Up; g.U0 = h->uoff;
     auto gemv = [&](const double* A, const double* x, double* y, double alpha, const double* C0,
                     double beta, int epi, double* red, bool gated) -> int {
+      if (gated && !refine) return GPK_OK;
       GemvDesc q = g;
       q.A = A; q.x = x; q.y = y; q.alpha = alpha; q.C0 = C0; q.beta = beta; q.epi = epi; q.red = red;
       q.gate = gated ? h->pst[0] : nullptr;
@@ -343,7 +357,7 @@ static int enqueue_step(gpk_handle* h, int apply) {
     pa.x = h->x1; pa.n = L.n1; pa.p = P; pa.kc = h->kc;
     pa.Kinv = h->Kinv[0]; pa.alpha = h->alpha; pa.beta = h->beta; pa.R = h->R;
     pa.halfc = 0.5 * h->prob.logdet; pa.deriv = 2; pa.part = h->pgpart;
-    TailArgs tail = make_tail(h, apply);
+    TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 1, &pa, 1, h->bpa, h->sc, h->s, &tail), "pgrad"));
     mark(h, stage++);
   }
@@ -372,6 +386,8 @@ static int build_descs(gpk_handle* h) {
   const int force_big = gemm_force(h->prob.flags);
   auto end = [&](int k) {
     h->st[k].n = (int)d.size() - h->st[k].off;
+    h->st[k].gated = h->st[k].n > 0;
+    for (int i = h->st[k].off; i < (int)d.size(); ++i) h->st[k].gated &= d[i].gate != nullptr;
     h->st[k].variant = gemm_variant(d.data() + h->st[k].off, h->st[k].n, force_big);
   };
   // Every solve against K (JAX: LU solves, model_GP_solver_2d.py:104-105 and the reverse
@@ -729,20 +745,21 @@ static int enqueue_step_shard(gpk_handle* h, int apply) {
   return GPK_OK;
 }
 
-static int capture(gpk_handle* h, int apply) {
-  if (h->g_exec[apply]) return GPK_OK;
+static int capture(gpk_handle* h, int apply, bool refine = true) {
+  hipGraphExec_t* slot = refine ? &h->g_exec[apply] : &h->g_fast[apply];
+  if (*slot) return GPK_OK;
   if (h->shard && !h->comm->capturable())
     return fail(GPK_EINVAL, "handle belongs to an in-process rank group: use gpk_group_step / gpk_group_loss_grad");
   hipGraph_t g = nullptr;
   HIPCHK(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
-  int rc = enqueue_step(h, apply);
+  int rc = enqueue_step(h, apply, refine);
   hipError_t e = hipStreamEndCapture(h->s, &g);
   if (rc != GPK_OK) {
     if (g) (void)hipGraphDestroy(g);
     return rc;
   }
   if (e != hipSuccess) return fail(GPK_EHIP, std::string("capture: ") + hipGetErrorString(e));
-  e = hipGraphInstantiate(&h->g_exec[apply], g, nullptr, nullptr, 0);
+  e = hipGraphInstantiate(slot, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   if (e != hipSuccess) return fail(GPK_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
   return GPK_OK;
@@ -755,6 +772,35 @@ static int read_status(gpk_handle* h) {
   if (st) {
     HIPCHK(hipMemsetAsync(h->status, 0, sizeof(int), h->s));
     return fail(GPK_ENOTPD, "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
+  }
+  return GPK_OK;
+}
+
+// End of a batch (one synchronisation): non-positive-definite status, the fast graph's gate
+// violation flag, and the refinement gate of the last step, which picks the next batch's graph:
+// the fast one while max_a K00 * max diag K_a^{-1} stays 8x below REFINE_COND_LB.  The gate
+// moves slowly (a few percent per Adam step), and a step that crosses it anyway is caught by
+// the check in the fast graph's tail (viol) and rerun.
+constexpr double FAST_GRAPH_MARGIN = 8.0;
+static int finish_batch(gpk_handle* h, bool fast, bool* violated) {
+  int st = 0;
+  unsigned int vi = 0;
+  double ps[2][2] = {};
+  HIPCHK(hipMemcpyAsync(&st, h->status, sizeof(int), hipMemcpyDeviceToHost, h->s));
+  if (fast) HIPCHK(hipMemcpyAsync(&vi, h->viol, sizeof(unsigned int), hipMemcpyDeviceToHost, h->s));
+  for (int a = 0; a < h->L.naxes; ++a)
+    HIPCHK(hipMemcpyAsync(ps[a], h->pst[a], 2 * sizeof(double), hipMemcpyDeviceToHost, h->s));
+  HIPCHK(hipStreamSynchronize(h->s));
+  *violated = false;
+  if (st) {
+    HIPCHK(hipMemsetAsync(h->status, 0, sizeof(int), h->s));
+    return fail(GPK_ENOTPD, "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
+  }
+  *violated = fast && vi;
+  if (h->fast_ok) {
+    double lb = 0.0;  // pst[a][1] holds max diag K^{-1} (positive, atomicMax'd as its bits)
+    for (int a = 0; a < h->L.naxes; ++a) lb = std::max(lb, ps[a][0] * ps[a][1]);
+    h->fast_mode = !*violated && lb * FAST_GRAPH_MARGIN < REFINE_COND_LB;
   }
   return GPK_OK;
 }
@@ -987,6 +1033,9 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   A_(h->ttop, 1);
   A_(h->tgpart, (size_t)L.naxes * h->tngpa * 3 * QMAX);
   A_(h->bgap, 1);
+  A_(h->snap, (size_t)3 * L.nparams);
+  A_(h->snap_count, 1);
+  A_(h->viol, 1);
 #undef A_
   // upload the problem
   if (hipMemcpyAsync(h->x1, p->x1, L.n1 * sizeof(double), hipMemcpyHostToDevice, h->s) != hipSuccess)
@@ -1016,6 +1065,8 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   }
   if (L.dim == 2 && (rc = build_descs(h)) != GPK_OK) return bail(rc);
   if (shard && (rc = build_shard(h)) != GPK_OK) return bail(rc);
+  h->fast_ok = !shard && !(p->flags & GPK_FLAG_NO_FAST_GRAPH);
+  h->fast_mode = h->fast_ok && (p->flags & GPK_FLAG_FAST_FIRST);
   *out = h;
   return GPK_OK;
 }
@@ -1155,8 +1206,10 @@ int gpk_destroy(gpk_handle* h) {
   if (!h) return GPK_OK;
   DevSwitch ds(h->dev);
   if (h->s) (void)hipStreamSynchronize(h->s);
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < 2; ++k) {
     if (h->g_exec[k]) (void)hipGraphExecDestroy(h->g_exec[k]);
+    if (h->g_fast[k]) (void)hipGraphExecDestroy(h->g_fast[k]);
+  }
   for (int k = 0; k <= kMaxStages; ++k)
     if (h->ev[k]) (void)hipEventDestroy(h->ev[k]);
   for (void* p : h->allocs) (void)hipFree(p);
@@ -1179,6 +1232,8 @@ int gpk_set_params(gpk_handle* h, const double* flat, int64_t n) {
   HIPCHK(hipMemcpyAsync(h->params, flat, n * sizeof(double), hipMemcpyHostToDevice, h->s));
   TRY(check_launch(launch_sync_u(h->params, h->L, h->Up, h->s), "sync_u"));
   HIPCHK(hipStreamSynchronize(h->s));
+  // new parameters: the next batch runs the full graph until their gate value has been seen
+  h->fast_mode = h->fast_ok && (h->prob.flags & GPK_FLAG_FAST_FIRST);
   return GPK_OK;
 }
 
@@ -1222,30 +1277,73 @@ int gpk_get_opt_state(gpk_handle* h, int64_t* count, double* mu, double* nu, int
 int gpk_loss_grad(gpk_handle* h, double* loss, double* grad_flat) {
   if (!h || !loss) return fail(GPK_EINVAL, "NULL argument");
   DevSwitch ds(h->dev);
-  TRY(capture(h, 0));
-  HIPCHK(hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s));
-  HIPCHK(hipGraphLaunch(h->g_exec[0], h->s));
-  HIPCHK(hipMemcpyAsync(loss, h->diag, sizeof(double), hipMemcpyDeviceToHost, h->s));
-  if (grad_flat)
-    HIPCHK(hipMemcpyAsync(grad_flat, h->grad, h->L.nparams * sizeof(double), hipMemcpyDeviceToHost, h->s));
-  return read_status(h);
+  bool fast = h->fast_ok && h->fast_mode, viol = false;
+  for (int pass = 0; pass < 2; ++pass) {
+    TRY(capture(h, 0, !fast));
+    if (fast) HIPCHK(hipMemsetAsync(h->viol, 0, sizeof(unsigned int), h->s));
+    HIPCHK(hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s));
+    HIPCHK(hipGraphLaunch(fast ? h->g_fast[0] : h->g_exec[0], h->s));
+    HIPCHK(hipMemcpyAsync(loss, h->diag, sizeof(double), hipMemcpyDeviceToHost, h->s));
+    if (grad_flat)
+      HIPCHK(hipMemcpyAsync(grad_flat, h->grad, h->L.nparams * sizeof(double), hipMemcpyDeviceToHost, h->s));
+    TRY(finish_batch(h, fast, &viol));
+    if (!viol) break;
+    ++h->rollbacks;  // nothing to restore: apply = 0 leaves params and Adam state alone
+    fast = false;
+  }
+  return GPK_OK;
+}
+
+static int run_steps(gpk_handle* h, int n_steps, double* losses, bool fast) {
+  hipGraphExec_t ge = fast ? h->g_fast[1] : h->g_exec[1];
+  int done = 0;
+  while (done < n_steps) {
+    const int nb = std::min(LOSS_CAP, n_steps - done);
+    HIPCHK(hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s));
+    for (int i = 0; i < nb; ++i) HIPCHK(hipGraphLaunch(ge, h->s));
+    if (losses)
+      HIPCHK(hipMemcpyAsync(losses + done, h->losses, nb * sizeof(double), hipMemcpyDeviceToHost, h->s));
+    done += nb;
+  }
+  return GPK_OK;
 }
 
 int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
   if (!h) return fail(GPK_EINVAL, "NULL handle");
   if (n_steps < 0) return fail(GPK_EINVAL, "n_steps < 0");
   DevSwitch ds(h->dev);
-  TRY(capture(h, 1));
-  int done = 0;
-  while (done < n_steps) {
-    const int nb = std::min(LOSS_CAP, n_steps - done);
-    HIPCHK(hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s));
-    for (int i = 0; i < nb; ++i) HIPCHK(hipGraphLaunch(h->g_exec[1], h->s));
-    if (losses)
-      HIPCHK(hipMemcpyAsync(losses + done, h->losses, nb * sizeof(double), hipMemcpyDeviceToHost, h->s));
-    done += nb;
+  const bool fast = h->fast_ok && h->fast_mode && n_steps > 0;
+  TRY(capture(h, 1, !fast));
+  const size_t np = (size_t)h->L.nparams, nb = np * sizeof(double);
+  if (fast) {  // snapshot of everything a step carries forward (Up is rebuilt from params)
+    HIPCHK(hipMemcpyAsync(h->snap, h->params, nb, hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemcpyAsync(h->snap + np, h->m, nb, hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemcpyAsync(h->snap + 2 * np, h->v, nb, hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemcpyAsync(h->snap_count, h->count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemsetAsync(h->viol, 0, sizeof(unsigned int), h->s));
   }
-  return read_status(h);
+  TRY(run_steps(h, n_steps, losses, fast));
+  bool viol = false;
+  TRY(finish_batch(h, fast, &viol));
+  if (viol) {  // a step of the batch needed refinement: roll back and rerun with the full graph
+    ++h->rollbacks;
+    HIPCHK(hipMemcpyAsync(h->params, h->snap, nb, hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemcpyAsync(h->m, h->snap + np, nb, hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemcpyAsync(h->v, h->snap + 2 * np, nb, hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemcpyAsync(h->count, h->snap_count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
+    TRY(check_launch(launch_sync_u(h->params, h->L, h->Up, h->s), "sync_u"));
+    TRY(capture(h, 1, true));
+    TRY(run_steps(h, n_steps, losses, false));
+    TRY(finish_batch(h, false, &viol));
+  }
+  return GPK_OK;
+}
+
+int gpk_graph_mode(const gpk_handle* h, int32_t* fast, int64_t* rollbacks) {
+  if (!h) return fail(GPK_EINVAL, "NULL handle");
+  if (fast) *fast = (h->fast_ok && h->fast_mode) ? 1 : 0;
+  if (rollbacks) *rollbacks = h->rollbacks;
+  return GPK_OK;
 }
 
 int gpk_criterion(gpk_handle* h, double* out) {

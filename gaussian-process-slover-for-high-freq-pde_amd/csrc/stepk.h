@@ -37,6 +37,10 @@ struct FinalizeArgs {
   double* losses; int* loss_slot;
   double* diag;              // [8]: loss, logdet1, logdet2, quad, egap, bgap
   const double* bgap;        // [1] ||u_b - b||^2 at the start of the step (assembly launch)
+  // fast graph (refinement stages left out): the refinement gate of each axis is checked here
+  // and an open one raises *viol, after which the host rolls the batch back and reruns it
+  // with the refinement stages (gpk_step).  watch[a] = nullptr: not checked.
+  const double* watch[2]; unsigned int* viol;
 };
 
 struct AdamUArgs {

@@ -39,6 +39,9 @@ __device__ inline void finalize_body(const FinalizeArgs& f) {
   quad = block_sum(quad, sh);
   egap = block_sum(egap, sh);
   bgap = *f.bgap;  // boundary gap of U at the start of the step (assembly launch)
+  if (t == 0 && f.viol)
+    for (int a = 0; a < L.naxes; ++a)
+      if (f.watch[a] && gate_open(f.watch[a])) atomicOr(f.viol, 1u);
 
   const double tau = f.sc->tau, v = f.sc->v;
   const double log_tau = f.params[L.off_tau], log_v = f.params[L.off_v];

@@ -16,6 +16,8 @@ GPK_FLAG_FORCE_BIG_GEMM = 1  # include/gpk.h
 GPK_FLAG_FORCE_BIG_SPD = 2
 GPK_FLAG_FORCE_SMALL_SPD = 4
 GPK_FLAG_FORCE_HUGE_GEMM = 8
+GPK_FLAG_NO_FAST_GRAPH = 16
+GPK_FLAG_FAST_FIRST = 32
 KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}
 EQ_IDS = {"poisson": 0, "allencahn": 1, "advection": 2}
 
@@ -83,6 +85,7 @@ EXPORTS = {
     "gpk_group_step": ([ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_int32, _dp], ctypes.c_int),
     "gpk_group_loss_grad": ([ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, _dp, _dp], ctypes.c_int),
     "gpk_shard_info": ([ctypes.c_void_p, _ip, _ip, _ip, _ip], ctypes.c_int),
+    "gpk_graph_mode": ([ctypes.c_void_p, _ip, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
 }
 
 _LIB = None

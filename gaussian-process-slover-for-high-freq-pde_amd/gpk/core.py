@@ -117,6 +117,13 @@ class DeviceSolver:
         check(_lib.load().gpk_shard_info(self._h, *[ctypes.byref(x) for x in v]))
         return tuple(int(x.value) for x in v)
 
+    def graph_mode(self):
+        """(fast, rollbacks): whether the next step runs the graph without the refinement
+        stages, and how many batches were rolled back and rerun with the full graph."""
+        f, r = ctypes.c_int32(), ctypes.c_int64()
+        check(_lib.load().gpk_graph_mode(self._h, ctypes.byref(f), ctypes.byref(r)))
+        return bool(f.value), int(r.value)
+
     # -- lifecycle ---------------------------------------------------------------------
     def close(self):
         if getattr(self, "_h", None):

@@ -82,6 +82,14 @@ typedef struct gpk_problem {
 #define GPK_FLAG_FORCE_BIG_SPD 2  /* use the 64-wide panel/update SPD inverse at every size */
 #define GPK_FLAG_FORCE_SMALL_SPD 4 /* use the 32-wide sweep SPD inverse at every size */
 #define GPK_FLAG_FORCE_HUGE_GEMM 8 /* use the 128x128 throughput GEMM at every size (tests/tuning) */
+/* gpk_step / gpk_loss_grad run one of two captured step graphs: the full one, whose iterative-
+ * refinement GEMM stages check a device-side cond(K) gate and skip themselves when it is closed,
+ * or a fast one without those stages, chosen while the last observed gate value is 8x below its
+ * threshold.  The fast graph checks the gate every step; a step that needed refinement makes the
+ * call roll its batch back (params, Adam state) and rerun it with the full graph, so results are
+ * bitwise those of the full graph. */
+#define GPK_FLAG_NO_FAST_GRAPH 16  /* always run the full graph */
+#define GPK_FLAG_FAST_FIRST 32     /* start in fast-graph mode (tests: exercises the rollback) */
 
 typedef struct gpk_handle gpk_handle;
 
@@ -112,6 +120,10 @@ int gpk_kernel_pairs(int32_t kind, int32_t deriv, const double* x1, const double
  * state.  freq_scale sets the initial frequencies linspace(0,1,Q)*freq_scale. */
 int gpk_create(const gpk_problem* prob, double freq_scale, gpk_handle** out);
 int gpk_destroy(gpk_handle* h);
+
+/* Graph selection state (see GPK_FLAG_NO_FAST_GRAPH): *fast = 1 if the next gpk_step uses the
+ * fast graph, *rollbacks = batches rerun with the full graph so far.  Either pointer may be NULL. */
+int gpk_graph_mode(const gpk_handle* h, int32_t* fast, int64_t* rollbacks);
 
 /* Flat parameter layout = jax's pytree leaf order (dict keys sorted):
  *   2D: [U (n1*n2, row-major), k1.freq[Q], k1.log-ls[Q], k1.log-w[Q],

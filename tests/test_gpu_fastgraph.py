@@ -1,0 +1,97 @@
+"""GPU: the fast step graph (refinement GEMM stages left out while the cond(K) gate is closed with
+margin, include/gpk.h GPK_FLAG_NO_FAST_GRAPH) is bitwise the full graph, and a fast batch that
+meets an open gate is rolled back and rerun with the full graph.
+
+The reference has no such switch (its LU solves are unrefined); the oracle-parity tests in
+test_gpu_parity.py pin the full graph, and these tests pin the fast graph to it bit for bit."""
+import numpy as np
+import pytest
+
+from oracle import gp_oracle as O
+from tests.helpers import device_solver, problem_1d, problem_2d
+
+pytestmark = pytest.mark.gpu
+
+
+def _gate_lb(prob, params):
+    """max over axes of K00 * max diag K^{-1}: the device's cond(K) lower bound (gpk_internal.h)."""
+    if "x" in prob:
+        axes = [(prob["x"], params["kernel_paras"])]
+    else:
+        axes = [(prob["x1"], params["kernel_paras_1"]), (prob["x2"], params["kernel_paras_2"])]
+    out = 0.0
+    for x, kp in axes:
+        K = O.kernel_matrix(prob["kind"], x, kp, prob["jitter"])
+        out = max(out, K[0, 0] * float(np.max(np.diag(np.linalg.inv(K)))))
+    return out
+
+
+def _case(name):
+    if name == "2d_closed":
+        prob, params, _, fs = problem_2d(n1=48, n2=40, Q=8, seed=6)
+    elif name == "2d_open":
+        prob, params, _, fs = problem_2d(eq="allencahn", kind="Matern52_1d", n1=40, n2=36, Q=5, seed=4)
+    elif name == "1d_closed":
+        prob, params, _ = problem_1d(n=64, Q=8, seed=6)
+        fs = 20.0
+    else:
+        prob, params, _ = problem_1d(kind="SE_1d", n=40, Q=5, seed=1)
+        fs = 20.0
+    kp = params.get("kernel_paras", params.get("kernel_paras_1"))
+    return prob, params, len(kp["freq"]), fs
+
+
+def _state(s):
+    cnt, mu, nu = s.get_opt_state()
+    return s.get_flat(), cnt, mu, nu
+
+
+@pytest.mark.parametrize("name", ["2d_closed", "1d_closed"])
+def test_fast_graph_bitwise_full(name):
+    from gpk._lib import GPK_FLAG_NO_FAST_GRAPH
+    prob, params, Q, fs = _case(name)
+    assert _gate_lb(prob, params) * 8 < 100  # precondition: gate closed with margin
+    full = device_solver(prob, Q, fs, flags=GPK_FLAG_NO_FAST_GRAPH)
+    fast = device_solver(prob, Q, fs)
+    for s in (full, fast):
+        s.set_params(params)
+    assert fast.graph_mode() == (False, 0)  # new params: full graph until the gate is seen
+    for b in range(4):
+        l_full, l_fast = full.step(3), fast.step(3)
+        assert np.array_equal(l_full, l_fast), b
+        assert fast.graph_mode() == (True, 0)
+        assert full.graph_mode()[0] is False
+    for a, b in zip(_state(full), _state(fast)):
+        assert np.array_equal(a, b)
+    lf, gf = full.loss_grad()
+    lq, gq = fast.loss_grad()
+    assert lf == lq and np.array_equal(gf, gq)
+    full.close()
+    fast.close()
+
+
+@pytest.mark.parametrize("name", ["2d_open", "1d_open"])
+def test_fast_graph_rollback(name):
+    from gpk._lib import GPK_FLAG_FAST_FIRST, GPK_FLAG_NO_FAST_GRAPH
+    prob, params, Q, fs = _case(name)
+    assert _gate_lb(prob, params) > 100  # precondition: refinement needed
+    full = device_solver(prob, Q, fs, flags=GPK_FLAG_NO_FAST_GRAPH)
+    fast = device_solver(prob, Q, fs, flags=GPK_FLAG_FAST_FIRST)
+    for s in (full, fast):
+        s.set_params(params)
+    assert fast.graph_mode() == (True, 0)
+    # loss_grad in fast mode meets the open gate: rerun with the full graph, nothing to restore
+    lf, gf = full.loss_grad()
+    lq, gq = fast.loss_grad()
+    assert lf == lq and np.array_equal(gf, gq)
+    assert fast.graph_mode() == (False, 1)
+    fast.set_params(params)  # FAST_FIRST: back to fast mode
+    l_full, l_fast = full.step(4), fast.step(4)
+    assert np.array_equal(l_full, l_fast)
+    assert fast.graph_mode() == (False, 2)  # rolled back once more, then stays on the full graph
+    for a, b in zip(_state(full), _state(fast)):
+        assert np.array_equal(a, b)
+    assert np.array_equal(full.step(2), fast.step(2))
+    assert fast.graph_mode() == (False, 2)
+    full.close()
+    fast.close()
