@@ -135,6 +135,9 @@ struct gpk_handle {
 
   hipGraphExec_t g_exec[2] = {nullptr, nullptr};  // [apply] full step graph
   hipGraphExec_t g_fast[2] = {nullptr, nullptr};  // [apply] without the refinement stages
+  // STEP_GRAPH_REPS training steps back to back in one graph ([0] fast, [1] full): one host
+  // launch per group of steps (a graph launch boundary costs ~5-9 us of idle GPU)
+  hipGraphExec_t g_multi[2] = {nullptr, nullptr};
   bool fast_ok = false;    // the fast graph exists for this handle (not row-sharded)
   int fast_mode = 0;       // next step(s) run the fast graph (gate closed with margin last time)
   long long rollbacks = 0;
@@ -745,14 +748,17 @@ static int enqueue_step_shard(gpk_handle* h, int apply) {
   return GPK_OK;
 }
 
-static int capture(gpk_handle* h, int apply, bool refine = true) {
-  hipGraphExec_t* slot = refine ? &h->g_exec[apply] : &h->g_fast[apply];
+constexpr int STEP_GRAPH_REPS = 8;
+static int capture(gpk_handle* h, int apply, bool refine = true, int reps = 1) {
+  hipGraphExec_t* slot = reps > 1 ? &h->g_multi[refine ? 1 : 0]
+                                  : refine ? &h->g_exec[apply] : &h->g_fast[apply];
   if (*slot) return GPK_OK;
   if (h->shard && !h->comm->capturable())
     return fail(GPK_EINVAL, "handle belongs to an in-process rank group: use gpk_group_step / gpk_group_loss_grad");
   hipGraph_t g = nullptr;
   HIPCHK(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
-  int rc = enqueue_step(h, apply, refine);
+  int rc = GPK_OK;
+  for (int r = 0; r < reps && rc == GPK_OK; ++r) rc = enqueue_step(h, apply, refine);
   hipError_t e = hipStreamEndCapture(h->s, &g);
   if (rc != GPK_OK) {
     if (g) (void)hipGraphDestroy(g);
@@ -1209,6 +1215,7 @@ int gpk_destroy(gpk_handle* h) {
   for (int k = 0; k < 2; ++k) {
     if (h->g_exec[k]) (void)hipGraphExecDestroy(h->g_exec[k]);
     if (h->g_fast[k]) (void)hipGraphExecDestroy(h->g_fast[k]);
+    if (h->g_multi[k]) (void)hipGraphExecDestroy(h->g_multi[k]);
   }
   for (int k = 0; k <= kMaxStages; ++k)
     if (h->ev[k]) (void)hipEventDestroy(h->ev[k]);
@@ -1296,11 +1303,17 @@ int gpk_loss_grad(gpk_handle* h, double* loss, double* grad_flat) {
 
 static int run_steps(gpk_handle* h, int n_steps, double* losses, bool fast) {
   hipGraphExec_t ge = fast ? h->g_fast[1] : h->g_exec[1];
+  const bool multi = !h->shard && n_steps >= STEP_GRAPH_REPS;
+  if (multi) TRY(capture(h, 1, !fast, STEP_GRAPH_REPS));
+  hipGraphExec_t gm = multi ? h->g_multi[fast ? 0 : 1] : nullptr;
   int done = 0;
   while (done < n_steps) {
     const int nb = std::min(LOSS_CAP, n_steps - done);
     HIPCHK(hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s));
-    for (int i = 0; i < nb; ++i) HIPCHK(hipGraphLaunch(ge, h->s));
+    int i = 0;
+    if (multi)
+      for (; i + STEP_GRAPH_REPS <= nb; i += STEP_GRAPH_REPS) HIPCHK(hipGraphLaunch(gm, h->s));
+    for (; i < nb; ++i) HIPCHK(hipGraphLaunch(ge, h->s));
     if (losses)
       HIPCHK(hipMemcpyAsync(losses + done, h->losses, nb * sizeof(double), hipMemcpyDeviceToHost, h->s));
     done += nb;

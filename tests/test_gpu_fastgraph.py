@@ -95,3 +95,21 @@ def test_fast_graph_rollback(name):
     assert fast.graph_mode() == (False, 2)
     full.close()
     fast.close()
+
+
+@pytest.mark.parametrize("name", ["2d_closed", "2d_open", "1d_closed"])
+def test_multi_step_graph_bitwise_single(name):
+    """Batches of >= 8 steps run graphs of 8 captured steps (+ single-step graphs for the
+    remainder): bitwise the same trajectory as one graph launch per step."""
+    prob, params, Q, fs = _case(name)
+    a = device_solver(prob, Q, fs)
+    b = device_solver(prob, Q, fs)
+    for s in (a, b):
+        s.set_params(params)
+    la = np.concatenate([a.step(2), a.step(19), a.step(16)])
+    lb = np.concatenate([b.step(1) for _ in range(37)])
+    assert np.array_equal(la, lb)
+    for x, y in zip(_state(a), _state(b)):
+        assert np.array_equal(x, y)
+    a.close()
+    b.close()
