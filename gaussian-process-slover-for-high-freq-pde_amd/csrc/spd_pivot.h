@@ -20,125 +20,115 @@ __device__ __forceinline__ double rsqrt_f64(double p) {
 // full symmetric storage; clobbered) and M = L^{-1} (LDS out, stride SP); returns log det A in
 // thread 0 (and every thread < 64).
 //
-// Blocked right-looking, 4-column blocks B (8 block steps, one barrier each).  Thread t owns
-// column c = t&31, rows i = (t>>5) + 8r (r = 0..3) of A and of M, in registers.  Per block,
-// every thread factors the 4x4 diagonal block D = L_D L_D^T itself (W = L_D^{-1}; redundant
-// but communication-free), then
-//   l_iB = A_iB W^T,  l_cB = A_cB W^T                     (panel rows it needs)
-//   A_ic -= l_iB . l_cB          (i, c below B)           (trailing update, its elements)
-//   X_B = W M_B,c ;  M_ic -= l_iB . X_B  (i below B),  M_Bc = X_B  (final rows of L^{-1})
-// and publishes its updated elements through LDS.  Writes never change a value read in the
-// same block step (rows/columns of B and of earlier blocks are final), so one barrier per block
-// suffices.  The 4x4 square roots use v_rsq_f64 + two Newton steps (no fp64 sqrt/div
-// sequences).  Measured 7.0 us vs 12.5 us for the unblocked one-column-per-barrier form
-// (tools/probes/pivot1w_probe.hip); results agree to 3e-13 relative (M K M^T = I to 3e-13).
+// Blocked right-looking, 4-column blocks B (8 block steps, one barrier each), with the rank-4
+// trailing updates of A and of M on v_mfma_f64_16x16x4 (k = 4 = the block width).  Wave
+// (wr, wc) keeps the 16x16 quadrant (rows 16wr.., cols 16wc..) of A and of M in two MFMA
+// accumulators for the whole factorisation (lane: rows 16wr + lk + 4r, column 16wc + li).  Per
+// block every lane factors the 4x4 diagonal block D = L_D L_D^T itself (W = L_D^{-1}; redundant
+// but communication-free), then forms the three operand values it owns:
+//   A operand  -l_iB[lk] = -(A_iB W^T)[lk]       (i = 16wr + li, zero unless i is below B)
+//   B operand   l_cB[lk] =  (A_cB W^T)[lk]       (c = 16wc + li, zero unless c is below B)
+//   B operand   X[lk][c] =  (W M_B)[lk][c]
+// and one MFMA each gives A_ic -= l_iB . l_cB and M_ic -= l_iB . X_B (rows below B); the rows of
+// B become M_B = X.  Only entries that change are published to LDS, and the entries read in a
+// block step (A's column block B and diagonal block, M's rows B) never change in it, so one
+// barrier per block suffices and M needs no second buffer.  The 4x4 square roots use
+// v_rsq_f64 + two Newton steps.  Results are bitwise those of the VALU form it replaced (MFMA
+// f64 accumulates the 4 products in the same order); 5.2 us vs 6.6 us per factorisation
+// (tools/probes/pivot_mfma_probe.hip).
 // LP: the LDS pointer type -- plain double* when inlined into a kernel (address space inferred),
 // lds_ptr (address_space(3)) when called through a non-inlined function, so that the callee
 // still issues ds_read / ds_write instead of flat memory instructions.
 template <int BS = 4, typename LP = double*>
 __device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t, int* status) {
-  const int c = t & 31, i0 = t >> 5;
-  double a[4], m[4];
+  static_assert(BS == 4, "the MFMA update is rank 4");
+  typedef double dv4 __attribute__((ext_vector_type(4)));
+  const int lane = t & 63, wv = t >> 6, wr = wv >> 1, wc = wv & 1;
+  const int li = lane & 15, lk = lane >> 4;
+  const int ri = 16 * wr + li, cj = 16 * wc + li;
+  dv4 accA, accM;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    a[r] = A[(i0 + 8 * r) * SP + c];
-    m[r] = (i0 + 8 * r == c) ? 1.0 : 0.0;
-    M[(i0 + 8 * r) * SP + c] = m[r];
+    const int row = 16 * wr + lk + 4 * r;
+    accA[r] = A[row * SP + cj];
+    accM[r] = (row == cj) ? 1.0 : 0.0;
+    M[row * SP + cj] = accM[r];
   }
+  // (0/1 weights select row lk of W: a select chain on lk becomes a scratch-indexed array)
+  const double s0 = lk == 0 ? 1.0 : 0.0, s1 = lk == 1 ? 1.0 : 0.0, s2 = lk == 2 ? 1.0 : 0.0,
+               s3 = lk == 3 ? 1.0 : 0.0;
   __syncthreads();
 #pragma unroll
-  for (int kb = 0; kb < 32 / BS; ++kb) {
-    const int b0 = BS * kb;
-    double D[BS][BS], aiB[4][BS], acB[BS], mB[BS];
+  for (int kb = 0; kb < 8; ++kb) {
+    const int b0 = 4 * kb;
+    double D[4][4], ar[4], ac[4], mb[4];
 #pragma unroll
-    for (int x = 0; x < BS; ++x)
+    for (int x = 0; x < 4; ++x)
 #pragma unroll
       for (int y = 0; y <= x; ++y) D[x][y] = A[(b0 + x) * SP + b0 + y];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int y = 0; y < BS; ++y) aiB[r][y] = A[(i0 + 8 * r) * SP + b0 + y];
-#pragma unroll
-    for (int y = 0; y < BS; ++y) {
-      acB[y] = A[c * SP + b0 + y];
-      mB[y] = M[(b0 + y) * SP + c];
+    for (int z = 0; z < 4; ++z) {
+      ar[z] = A[ri * SP + b0 + z];
+      ac[z] = A[cj * SP + b0 + z];
+      mb[z] = M[(b0 + z) * SP + cj];
     }
     // D = L_D L_D^T, rinv[x] = 1 / (L_D)_xx
-    double L[BS][BS], rinv[BS];
+    double L[4][4], rinv[4];
 #pragma unroll
-    for (int x = 0; x < BS; ++x) {
+    for (int x = 0; x < 4; ++x) {
       double s = D[x][x];
 #pragma unroll
       for (int z = 0; z < x; ++z) s = fma(-L[x][z], L[x][z], s);
       if (t == 0) pv[b0 + x] = s;
       rinv[x] = rsqrt_f64(s);
 #pragma unroll
-      for (int y = x + 1; y < BS; ++y) {
+      for (int y = x + 1; y < 4; ++y) {
         double q = D[y][x];
 #pragma unroll
         for (int z = 0; z < x; ++z) q = fma(-L[y][z], L[x][z], q);
         L[y][x] = q * rinv[x];
       }
     }
-    // W = L_D^{-1}: W_xx = rinv_x, W_yx = -rinv_y sum_{z=x}^{y-1} L_yz W_zx
-    double W[BS][BS];
+    // W = L_D^{-1}: W_xx = rinv_x, W_yx = -rinv_y sum_{z=x}^{y-1} L_yz W_zx, zero above
+    double W[4][4];
 #pragma unroll
-    for (int x = 0; x < BS; ++x) {
+    for (int x = 0; x < 4; ++x) {
       W[x][x] = rinv[x];
 #pragma unroll
-      for (int y = x + 1; y < BS; ++y) {
+      for (int y = x + 1; y < 4; ++y) {
         double q = 0.0;
 #pragma unroll
         for (int z = x; z < y; ++z) q = fma(L[y][z], W[z][x], q);
         W[y][x] = -q * rinv[y];
       }
+#pragma unroll
+      for (int y = 0; y < x; ++y) W[y][x] = 0.0;
     }
-    double lc[BS], X[BS];
+    double lr = 0.0, lc = 0.0, xv = 0.0;
 #pragma unroll
-    for (int x = 0; x < BS; ++x) {
-      double q = 0.0, u = 0.0;
-#pragma unroll
-      for (int z = 0; z <= x; ++z) {
-        q = fma(acB[z], W[x][z], q);
-        u = fma(W[x][z], mB[z], u);
-      }
-      lc[x] = q;
-      X[x] = u;
+    for (int z = 0; z < 4; ++z) {
+      const double w = fma(W[0][z], s0, fma(W[1][z], s1, fma(W[2][z], s2, W[3][z] * s3)));
+      lr = fma(ar[z], w, lr);
+      lc = fma(ac[z], w, lc);
+      xv = fma(w, mb[z], xv);
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {  // branch-free: compute, then select
-      const int i = i0 + 8 * r;
-      double li[BS];
-#pragma unroll
-      for (int x = 0; x < BS; ++x) {
-        double q = 0.0;
-#pragma unroll
-        for (int z = 0; z <= x; ++z) q = fma(aiB[r][z], W[x][z], q);
-        li[x] = q;
-      }
-      double na = a[r], nm = m[r], xb = 0.0;
-#pragma unroll
-      for (int x = 0; x < BS; ++x) {
-        na = fma(-li[x], lc[x], na);
-        nm = fma(-li[x], X[x], nm);
-        xb = (i == b0 + x) ? X[x] : xb;
-      }
-      const bool below = i >= b0 + BS, inB = (i >= b0) && !below;
-      a[r] = (below && c >= b0 + BS) ? na : a[r];
-      m[r] = below ? nm : (inB ? xb : m[r]);
-    }
+    const double opa = (ri >= b0 + 4) ? -lr : 0.0;
+    const double opb = (cj >= b0 + 4) ? lc : 0.0;
+    accA = __builtin_amdgcn_mfma_f64_16x16x4f64(opa, opb, accA, 0, 0, 0);
+    accM = __builtin_amdgcn_mfma_f64_16x16x4f64(opa, xv, accM, 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = i0 + 8 * r;
-      if (i >= b0 + BS) {
-        A[i * SP + c] = a[r];
-        M[i * SP + c] = m[r];
+      const int row = 16 * wr + lk + 4 * r;
+      if (16 * wr + 4 * r == b0) accM[r] = xv;  // rows of B: M_B = X (final; written at the end)
+      if (kb < 7 && row >= b0 + 4) {
+        if (cj >= b0 + 4) A[row * SP + cj] = accA[r];
+        M[row * SP + cj] = accM[r];
       }
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) M[(i0 + 8 * r) * SP + c] = m[r];
+  for (int r = 0; r < 4; ++r) M[(16 * wr + lk + 4 * r) * SP + cj] = accM[r];
   double ls = 0.0;
   if (t < 64) {
     const double pk = pv[t & 31];
