@@ -13,10 +13,15 @@
 // ~1150 workgroups) and summed in fixed order through LDS; per-axis constants (w, a, 2*pi*f)
 // sit in LDS.  Pads (i or j >= n) are written as identity (K) / zero (D) so the padded SPD
 // inverse stays block-diagonal.
+#include <algorithm>
+
 #include "gpk_internal.h"
 #include "spd_pivot.h"
+#include "gpk_trace.h"
 
 namespace gpk {
+
+GPK_TRACE_TU(assemble)
 
 // Partial sums over components c = c0, c0 + cs, ... (cs = stride) of K and D at one pair.
 template <bool MATERN, bool COS, int DERIV>
@@ -94,15 +99,28 @@ __device__ void publish_prep(const PrepArgs& P, int q) {
     // u_b = hstack(U[0,:], U[-1,:], U[:,0], U[:,-1]) (2D) / u[Xind] (1D); fixed-order sum
     double acc = 0.0;
     if (P.dim == 2) {
+      // 8 boundary entries per thread per pass, loads issued before the sums (one round trip
+      // for the usual 4N <= 2048 entries instead of one per entry)
       const int n1 = P.n1, n2 = P.n2, nb = 2 * n2 + 2 * n1;
-      for (int k = t; k < nb; k += blockDim.x) {
-        int i, j;
-        if (k < n2) { i = 0; j = k; }
-        else if (k < 2 * n2) { i = n1 - 1; j = k - n2; }
-        else if (k < 2 * n2 + n1) { i = k - 2 * n2; j = 0; }
-        else { i = k - 2 * n2 - n1; j = n2 - 1; }
-        const double r = P.Up[(size_t)i * P.p2 + j] - P.bvals[k];
-        acc += r * r;
+      for (int k0 = t; k0 < nb; k0 += 8 * blockDim.x) {
+        double uu[8], bb[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int k = k0 + r * blockDim.x;
+          const bool ok = k < nb;
+          int i, j;
+          if (k < n2) { i = 0; j = k; }
+          else if (k < 2 * n2) { i = n1 - 1; j = k - n2; }
+          else if (k < 2 * n2 + n1) { i = k - 2 * n2; j = 0; }
+          else { i = k - 2 * n2 - n1; j = n2 - 1; }
+          uu[r] = ok ? P.Up[(size_t)i * P.p2 + j] : 0.0;
+          bb[r] = ok ? P.bvals[k] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const double d = uu[r] - bb[r];
+          acc += d * d;
+        }
       }
     } else {
       for (int k = t; k < P.nb; k += blockDim.x) {
@@ -124,21 +142,24 @@ __device__ void publish_prep(const PrepArgs& P, int q) {
 // (vmcnt drain, agent release, counter add); the pivot workgroup polls (sc1), acquires,
 // reads the tile and runs the Cholesky + L^{-1} of pivot_init.  It is dispatched after those
 // 16 (highest blockIdx.x), so they are resident or done: no deadlock at any grid size.
-__device__ void pivot0(const AssembleArgs& A) {
+__device__ void pivot0(const AssembleArgs& A, unsigned need) {
   __shared__ double P[32 * SP], M[32 * SP], pv[32];
   const int t = threadIdx.x;
   if (t == 0) {
-    while (__hip_atomic_load(A.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ASM_SUB)
+    while (__hip_atomic_load(A.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
       __builtin_amdgcn_s_sleep(1);
     *A.flag = 0u;  // re-arm for the next step (no other user until then)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // see the released tile rows
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (blockIdx.x == 0) TR_HI(SLOT_PIVOT0_WAIT);
   }
   __syncthreads();
   for (int e = t; e < 1024; e += 256) P[(e >> 5) * SP + (e & 31)] = A.K[(size_t)(e >> 5) * A.p + (e & 31)];
   __syncthreads();
   const double k00 = P[0];
+  if (t == 0 && blockIdx.x == 0) TR_LO(SLOT_PIVOT0);
   const double ls = pivot_chol_inv_block(P, M, pv, t, A.status);
+  if (t == 0 && blockIdx.x == 0) TR_HI(SLOT_PIVOT0);
   for (int e = t; e < 1024; e += 256) A.piv[e] = M[(e >> 5) * SP + (e & 31)];
   if (t == 0) {
     A.ldet[0] = ls;
@@ -165,7 +186,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
   if (blockIdx.x == 0 && axis == 0) publish_prep(b.prep, q);
   __syncthreads();
   if (pivot_wg) {
-    pivot0(A);
+    pivot0(A, ASM_SUB);
     return;
   }
   int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
@@ -211,6 +232,111 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       atomicAdd(A.flag, 1u);
     }
+  }
+}
+
+// ---- class path (gpk_internal.h ClassArgs) -------------------------------------------------
+// Launch 1: kappa and its derivative field at every class distance.  One mixture component per
+// lane: half-wave h of wave w holds class 8*blockIdx.x + 2w + h, lane c its component c (and
+// c + 32, ...); the 32 terms are added by a fixed xor-butterfly (deterministic).  The latency
+// of one exp + sincos instead of q/4 of them in sequence.  Workgroup (0, 0) also publishes the
+// step constants (prep).
+template <bool MATERN, bool COS, int DERIV>
+__global__ __launch_bounds__(256) void class_eval_kernel(AssembleBatch b, int q) {
+  const int axis = blockIdx.y;
+  const ClassArgs& C = b.ax[axis].cls;
+  const int t = threadIdx.x;
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
+  if (t < q) axis_component(b.prep, axis, q, t, sw[t], sa[t], so[t]);
+  if (blockIdx.x == 0 && axis == 0) publish_prep(b.prep, q);
+  __syncthreads();
+  if (TR_FIRST) TR_LO(SLOT_CLASS_EVAL);
+  if (TR_LAST) TR_LO(SLOT_CEVAL_START);
+  const int c = t & 31, u = blockIdx.x * 8 + (t >> 5);
+  double kv = 0.0, dv = 0.0;
+  if (u < C.ncls) eval_kd_part<MATERN, COS, DERIV>(C.dist[u], sw, sa, so, c, 32, q, kv, dv);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    kv += __shfl_xor(kv, o, 64);
+    dv += __shfl_xor(dv, o, 64);
+  }
+  if (c == 0 && u < C.ncls) {
+    C.kval[u] = kv;
+    C.dval[u] = dv;
+  }
+  if (TR_FIRST) TR_HI(SLOT_CLASS_EVAL);
+  if (TR_LAST) TR_HI(SLOT_CEVAL_START);
+}
+
+// Launch 2: K (+ jitter), its kept copy and D of one 32x32 tile per workgroup, gathered from
+// the class values (pads: identity / zero); the workgroup of tile (0, 0) releases it to the
+// pivot-0 workgroup (the last one of the grid), which factors it as in assemble_kernel.
+// grid (naxes, 1 + tiles [+ 1]): dispatch order = tile (0,0) of every axis, the pivot workgroups
+// (which wait for it: dispatched after it, so no deadlock), then the other tiles.
+template <int DERIV>
+__global__ __launch_bounds__(256) void gather_kernel(AssembleBatch b) {
+  const int axis = blockIdx.x;
+  const AssembleArgs& A = b.ax[axis];
+  const int t = threadIdx.x;
+  if (TR_LAST) TR_LO(SLOT_GATHER_START);
+  const bool piv = b.pivot_x >= 0;
+  if (piv && blockIdx.y == 1) {
+    if (t == 0 && axis == 0) TR_LO(SLOT_GATHER);
+    pivot0(A, 1u);
+    if (t == 0 && axis == 0) TR_HI(SLOT_GATHER);
+    return;
+  }
+  const int T = A.p / 32;
+  const int tile = (piv && blockIdx.y > 1) ? (int)blockIdx.y - 1 : (int)blockIdx.y;
+  if (tile >= T * T) return;
+  if (tile == 0 && b.pivot_x >= 0) __builtin_amdgcn_s_setprio(3);
+  const int I = tile / T, J = tile % T;
+  const int j = J * 32 + (t & 31);
+  const ClassArgs& C = b.ax[axis].cls;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = I * 32 + (t >> 5) + 8 * r;
+    const size_t o = (size_t)i * A.p + j;
+    const int u = C.cid[o];
+    double kv, dv;
+    if (u >= 0) {
+      kv = C.kval[u];
+      if (i == j) kv += A.jitter;
+      dv = C.dval[u];
+      if (DERIV == 1 && !(A.x[i] - A.x[j] >= 0.0)) dv = -dv;  // JAX abs'(0) = +1
+    } else {
+      kv = (i == j) ? 1.0 : 0.0;
+      dv = 0.0;
+    }
+    A.K[o] = kv;
+    if (A.Kc) A.Kc[o] = kv;
+    if (DERIV) A.D[o] = dv;
+  }
+  if (tile == 0 && b.pivot_x >= 0) {  // release tile (0, 0) to pivot0
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      atomicAdd(A.flag, 1u);
+    }
+  }
+  if (TR_LAST) TR_HI(SLOT_GATHER_START);
+}
+
+template <bool MATERN, bool COS>
+static void launch_class_t(const AssembleBatch& b, int naxes, int maxc, int maxtiles, int q,
+                           int deriv, hipStream_t s, bool eval_only) {
+  dim3 ge((maxc + 7) / 8, naxes), gg(naxes, maxtiles + (b.pivot_x >= 0 ? 1 : 0));
+  if (deriv == 2) {
+    hipLaunchKernelGGL((class_eval_kernel<MATERN, COS, 2>), ge, dim3(256), 0, s, b, q);
+    if (!eval_only) hipLaunchKernelGGL((gather_kernel<2>), gg, dim3(256), 0, s, b);
+  } else if (deriv == 1) {
+    hipLaunchKernelGGL((class_eval_kernel<MATERN, COS, 1>), ge, dim3(256), 0, s, b, q);
+    if (!eval_only) hipLaunchKernelGGL((gather_kernel<1>), gg, dim3(256), 0, s, b);
+  } else {
+    hipLaunchKernelGGL((class_eval_kernel<MATERN, COS, 0>), ge, dim3(256), 0, s, b, q);
+    if (!eval_only) hipLaunchKernelGGL((gather_kernel<0>), gg, dim3(256), 0, s, b);
   }
 }
 
@@ -294,7 +420,7 @@ static void launch_assemble_t(const AssembleBatch& b, int naxes, int maxt, int q
 }
 
 hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, const PrepArgs& prep,
-                           hipStream_t s) {
+                           hipStream_t s, bool eval_only) {
   AssembleBatch b{};
   int maxt = 0;
   for (int k = 0; k < naxes; ++k) {
@@ -304,10 +430,28 @@ hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, co
     if (b.tiles[k] > maxt) maxt = b.tiles[k];
   }
   b.prep = prep;
-  b.pivot_x = a[0].piv ? maxt * ASM_SUB : -1;
   for (int k = 1; k < naxes; ++k)
-    if ((a[k].piv != nullptr) != (a[0].piv != nullptr)) return hipErrorInvalidValue;
+    if ((a[k].piv != nullptr) != (a[0].piv != nullptr) ||
+        (a[k].cls.ncls > 0) != (a[0].cls.ncls > 0))
+      return hipErrorInvalidValue;
   int deriv = a[0].deriv;
+  if (a[0].cls.ncls > 0) {  // class path: every 32x32 tile of the full matrix, one per workgroup
+    int maxc = 0, maxtiles = 0;
+    for (int k = 0; k < naxes; ++k) {
+      const int T = a[k].p / 32;
+      maxtiles = std::max(maxtiles, T * T);
+      maxc = std::max(maxc, a[k].cls.ncls);
+    }
+    b.pivot_x = a[0].piv ? maxtiles : -1;
+    switch (kind) {
+      case SE_COS: launch_class_t<false, true>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
+      case MATERN52_COS: launch_class_t<true, true>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
+      case SE: launch_class_t<false, false>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
+      default: launch_class_t<true, false>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
+    }
+    return hipGetLastError();
+  }
+  b.pivot_x = a[0].piv ? maxt * ASM_SUB : -1;
   switch (kind) {
     case SE_COS: launch_assemble_t<false, true>(b, naxes, maxt, q, deriv, s); break;
     case MATERN52_COS: launch_assemble_t<true, true>(b, naxes, maxt, q, deriv, s); break;

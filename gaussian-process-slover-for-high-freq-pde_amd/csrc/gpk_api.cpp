@@ -27,6 +27,7 @@
 #include "../../include/gpk.h"
 #include "gpk_internal.h"
 #include "stepk.h"
+#include "gpk_trace.h"
 
 using namespace gpk;
 
@@ -119,6 +120,9 @@ struct gpk_handle {
   unsigned int* aflag[2] = {};        // assembly -> pivot-0 hand-off counters (small path) /
                                       // update -> pivot hand-off counters (large path)
   bool bigspd = false;                // large-factor SPD inverse (spdinv_big.hip)
+  bool chain = false;                 // small factors: persistent one-launch inverse (chain_kernel)
+  unsigned int* cflags[2] = {};       // its hand-off flags [T*T + T + 1] per factor
+  ClassArgs cls[2] = {};              // distance classes per axis (ncls = 0: per-pair path)
   double* rvec = nullptr;            // 1D refinement residual
   double* uoff = nullptr;            // 1D Allen-Cahn offset (gpk_problem.uoff), or null
   // predict scratch
@@ -218,10 +222,30 @@ static void fill_spd(gpk_handle* h, SpdArgs* sa) {
   }
 }
 
+// the persistent small-factor inverse; gather: K (+ Kc, D) straight from the distance classes
+static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin) {
+  const Layout& L = h->L;
+  ChainArgs ca[2] = {};
+  for (int a = 0; a < L.naxes; ++a) {
+    ChainArgs& c = ca[a];
+    c.X = h->K[a]; c.PB = h->Kb[a]; c.piv = h->piv[a]; c.ldet = h->ldet[a]; c.pst = h->pst[a];
+    c.status = h->status; c.flags = h->cflags[a];
+    c.p = a == 0 ? L.p1 : L.p2;
+    c.n = a == 0 ? L.n1 : L.n2;
+    if (gather) {
+      c.cid = h->cls[a].cid; c.kval = h->cls[a].kval; c.dval = h->cls[a].dval;
+      c.x = a == 0 ? h->x1 : h->x2; c.jitter = h->prob.jitter; c.Kc = h->Kc[a]; c.D = h->D[a];
+    }
+    fin[a] = h->K[a];
+  }
+  return launch_spd_chain(ca, L.naxes, h->prob.eq == GPK_ADVECTION ? 1 : 2, h->s);
+}
+
 // the SPD inverse of every factor (small: 32-wide sweeps, pivot 0 possibly fused into the
 // assembly launch; large: 64-wide panel/update sweeps)
 static hipError_t launch_inverse(gpk_handle* h, SpdArgs* sa, double** fin, bool pivot0_done) {
   if (h->bigspd) return launch_spd_inverse_big(sa, h->L.naxes, fin, h->s);
+  if (h->chain) return launch_chain(h, false, fin);
   return launch_spd_inverse(sa, h->L.naxes, fin, h->s, pivot0_done);
 }
 
@@ -240,7 +264,8 @@ static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
     aa[a].D = h->D[a];
     aa[a].deriv = deriv;
     aa[a].Kc = h->Kc[a];
-    if (!h->bigspd) {  // pivot block 0 factored inside the assembly launch (small path)
+    aa[a].cls = h->cls[a];
+    if (!h->bigspd && !h->chain) {  // pivot block 0 factored inside the assembly launch
       aa[a].piv = h->piv[a];
       aa[a].ldet = h->ldet[a];
       aa[a].pst = h->pst[a];
@@ -248,12 +273,18 @@ static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
       aa[a].flag = h->aflag[a];
     }
   }
-  TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, apply), h->s), "assemble"));
+  // chain + classes: the class values only; the inverse launch gathers K, Kc, D itself
+  const bool eval_only = h->chain && h->cls[0].ncls > 0;
+  TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, apply), h->s, eval_only),
+                   "assemble"));
   mark(h, 1);
   SpdArgs sa[2];
   fill_spd(h, sa);
   double* fin[2] = {nullptr, nullptr};
-  TRY(check_launch(launch_inverse(h, sa, fin, true), "spd_inverse"));
+  if (h->chain)
+    TRY(check_launch(launch_chain(h, eval_only, fin), "spd_chain"));
+  else
+    TRY(check_launch(launch_inverse(h, sa, fin, true), "spd_inverse"));
   for (int a = 0; a < L.naxes; ++a) h->Kinv[a] = fin[a];
   mark(h, 2);
   return GPK_OK;
@@ -318,6 +349,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
       pa[a].GD = h->GD[a];
       pa[a].deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
+      pa[a].cls = h->cls[a];
     }
     TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, &tail), "pgrad"));
@@ -359,13 +391,45 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
     PGradArgs pa{};
     pa.x = h->x1; pa.n = L.n1; pa.p = P; pa.kc = h->kc;
     pa.Kinv = h->Kinv[0]; pa.alpha = h->alpha; pa.beta = h->beta; pa.R = h->R;
-    pa.halfc = 0.5 * h->prob.logdet; pa.deriv = 2; pa.part = h->pgpart;
+    pa.halfc = 0.5 * h->prob.logdet; pa.deriv = 2; pa.part = h->pgpart; pa.cls = h->cls[0];
     TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 1, &pa, 1, h->bpa, h->sc, h->s, &tail), "pgrad"));
     mark(h, stage++);
   }
   h->nstage = stage;
   return GPK_OK;
+}
+
+// Distance classes of one axis (gpk_internal.h ClassArgs): per diagonal k the distinct exact
+// values of d = |x_{j+k} - x_j| (= |x_j - x_{j+k}| bitwise), in order of first appearance.
+// false: some diagonal has more than CLS_VMAX of them (the step keeps the per-pair kernels).
+static bool build_classes(const double* x, int n, int P, std::vector<double>& dist,
+                          std::vector<int>& cid, std::vector<int>& cbase, int& vmax) {
+  cid.assign((size_t)P * P, -1);
+  cbase.assign((size_t)n + 1, 0);
+  dist.clear();
+  vmax = 0;
+  double vals[CLS_VMAX];
+  for (int k = 0; k < n; ++k) {
+    int nv = 0;
+    cbase[k] = (int)dist.size();
+    for (int j = 0; j + k < n; ++j) {
+      const double d = std::fabs(x[j + k] - x[j]);
+      int v = 0;
+      while (v < nv && !(vals[v] == d)) ++v;
+      if (v == nv) {
+        if (nv == CLS_VMAX) return false;
+        vals[nv++] = d;
+        dist.push_back(d);
+      }
+      const int c = cbase[k] + v;
+      cid[(size_t)(j + k) * P + j] = c;
+      cid[(size_t)j * P + j + k] = c;
+    }
+    vmax = std::max(vmax, nv);
+  }
+  cbase[n] = (int)dist.size();
+  return true;
 }
 
 static int gemm_force(int flags) {
@@ -726,6 +790,7 @@ static int enqueue_step_shard(gpk_handle* h, int apply) {
     pa[a].GD = h->GD[a];
     pa[a].deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
     pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
+    pa[a].cls = h->cls[a];
   }
   TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, nullptr, h->rank,
                                 h->nranks), "pgrad"));
@@ -972,6 +1037,8 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     const int pmax = std::max(L.p1, L.dim == 2 ? L.p2 : 0);
     h->bigspd = (p->flags & GPK_FLAG_FORCE_BIG_SPD) != 0 ||
                 (!(p->flags & GPK_FLAG_FORCE_SMALL_SPD) && pmax >= SPD_BIG_MIN);
+    const int pp[2] = {L.p1, L.p2};
+    h->chain = !h->bigspd && !(p->flags & GPK_FLAG_NO_CHAIN) && spd_chain_ok(pp, L.naxes);
   }
   auto bail = [&](int rc) {
     gpk_destroy(h);
@@ -1011,6 +1078,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     A_(h->Kc[a], (size_t)P * P);
     A_(h->pst[a], 2);
     A_(h->aflag[a], 1);
+    A_(h->cflags[a], (size_t)(P / 32) * (P / 32) + P / 32 + 1);
     h->nldet[a] = P / 32;
   }
   if (L.dim == 2) {
@@ -1030,7 +1098,37 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   }
   A_(h->red_quad, h->nquad);
   A_(h->red_egap, h->negap);
-  h->bpa = std::max(pgrad_blocks(L.n1), L.dim == 2 ? pgrad_blocks(L.n2) : 0);
+  // distance classes (both axes or none), uploaded once: the coordinates never change
+  std::vector<double> cdist[2];
+  std::vector<int> ccid[2], cbase[2];
+  bool use_cls = !(p->flags & GPK_FLAG_NO_DCLASS);
+  int vmax[2] = {0, 0};
+  for (int a = 0; a < L.naxes && use_cls; ++a)
+    use_cls = build_classes(a == 0 ? p->x1 : p->x2, a == 0 ? L.n1 : L.n2, a == 0 ? P1 : P2,
+                            cdist[a], ccid[a], cbase[a], vmax[a]);
+  if (use_cls) {
+    for (int a = 0; a < L.naxes; ++a) {
+      const int P = a == 0 ? P1 : P2, U = (int)cdist[a].size();
+      ClassArgs& c = h->cls[a];
+      double *dist = nullptr, *kval = nullptr, *dval = nullptr, *part = nullptr;
+      int *cid = nullptr, *cb = nullptr;
+      // class-sum row chunks: <= 64 chunks of >= 16 rows (one 4-row group per wave and pass)
+      const int n = a == 0 ? L.n1 : L.n2;
+      const int rb = std::max(16, (n + 63) / 64 + 15) / 16 * 16;
+      const int nchunk = (n + rb - 1) / rb;
+      A_(dist, U); A_(kval, U); A_(dval, U); A_(part, (size_t)2 * nchunk * U);
+      A_(cid, (size_t)P * P); A_(cb, cbase[a].size());
+      if (hipMemcpyAsync(dist, cdist[a].data(), U * sizeof(double), hipMemcpyHostToDevice, h->s) != hipSuccess ||
+          hipMemcpyAsync(cid, ccid[a].data(), ccid[a].size() * sizeof(int), hipMemcpyHostToDevice, h->s) != hipSuccess ||
+          hipMemcpyAsync(cb, cbase[a].data(), cbase[a].size() * sizeof(int), hipMemcpyHostToDevice, h->s) != hipSuccess)
+        return bail(fail(GPK_EHIP, "upload distance classes"));
+      c.ncls = U; c.vmax = vmax[a]; c.dist = dist; c.cid = cid; c.cbase = cb;
+      c.kval = kval; c.dval = dval; c.nchunk = nchunk; c.rb = rb; c.part = part;
+    }
+    h->bpa = std::max(pgrad_class_blocks(h->cls[0].ncls), L.dim == 2 ? pgrad_class_blocks(h->cls[1].ncls) : 0);
+  } else {
+    h->bpa = std::max(pgrad_blocks(L.n1), L.dim == 2 ? pgrad_blocks(L.n2) : 0);
+  }
   A_(h->pgpart, (size_t)L.naxes * h->bpa * 3 * QMAX);
   A_(h->pg, (size_t)L.naxes * 3 * QMAX);
   h->ttg = std::max(32, (int)std::ceil(std::sqrt((double)h->bpa)));
@@ -1067,7 +1165,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   // of the inverse into a throwaway capture is unnecessary -- compute it directly.
   for (int a = 0; a < L.naxes; ++a) {
     const int T = (a == 0 ? P1 : P2) / 32;
-    h->Kinv[a] = h->bigspd ? h->K[a] : ((T & 1) ? h->Kb[a] : h->K[a]);
+    h->Kinv[a] = (h->bigspd || h->chain) ? h->K[a] : ((T & 1) ? h->Kb[a] : h->K[a]);
   }
   if (L.dim == 2 && (rc = build_descs(h)) != GPK_OK) return bail(rc);
   if (shard && (rc = build_shard(h)) != GPK_OK) return bail(rc);
@@ -1349,6 +1447,47 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
     TRY(run_steps(h, n_steps, losses, false));
     TRY(finish_batch(h, false, &viol));
   }
+  return GPK_OK;
+}
+
+int gpk_trace_reset(void) {
+  trace_reset_assemble();
+  trace_reset_spdinv();
+  trace_reset_pgrad();
+  return GPK_OK;
+}
+
+int gpk_trace_read(uint64_t* lo, uint64_t* hi, int32_t n) {
+  if (!lo || !hi || n < TRACE_SLOTS) return fail(GPK_EINVAL, "need 64 slots");
+  uint64_t l[3][TRACE_SLOTS], h[3][TRACE_SLOTS];
+  trace_fetch_assemble(l[0], h[0]);
+  trace_fetch_spdinv(l[1], h[1]);
+  trace_fetch_pgrad(l[2], h[2]);
+  for (int i = 0; i < TRACE_SLOTS; ++i) {
+    lo[i] = std::min(l[0][i], std::min(l[1][i], l[2][i]));
+    hi[i] = std::max(h[0][i], std::max(h[1][i], h[2][i]));
+  }
+#ifdef GPK_TRACE
+  return GPK_OK;
+#else
+  return fail(GPK_EINVAL, "built without GPK_TRACE (make trace -> libgpk_trace.so)");
+#endif
+}
+
+int gpk_distance_classes(const double* x, int32_t n, int32_t* ncls, int32_t* vmax) {
+  if (!x || n <= 0 || !ncls) return fail(GPK_EINVAL, "bad argument");
+  std::vector<double> dist;
+  std::vector<int> cid, cbase;
+  int vm = 0;
+  const bool ok = build_classes(x, n, pad_up(n), dist, cid, cbase, vm);
+  *ncls = ok ? (int32_t)dist.size() : 0;
+  if (vmax) *vmax = ok ? vm : CLS_VMAX + 1;
+  return GPK_OK;
+}
+
+int gpk_class_count(const gpk_handle* h, int32_t axis, int32_t* ncls) {
+  if (!h || !ncls || axis < 0 || axis >= h->L.naxes) return fail(GPK_EINVAL, "bad argument");
+  *ncls = h->cls[axis].ncls;
   return GPK_OK;
 }
 
@@ -1759,6 +1898,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
       pa[a].x = a == 0 ? h->x1 : h->x2; pa[a].n = a == 0 ? L.n1 : L.n2; pa[a].p = a == 0 ? L.p1 : L.p2;
       pa[a].kc = h->kc + a; pa[a].GK = h->GK[a]; pa[a].GD = h->GD[a]; pa[a].deriv = deriv;
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
+      pa[a].cls = h->cls[a];
     }
     launch = [&, pa]() mutable { return launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s); };
     bytes = 16.0 * (n1 * n1 + n2 * n2);  // G_K, G_D read

@@ -101,6 +101,31 @@ struct PrepArgs {
   double* bgap;        // out [1]
 };
 
+// Distance classes.  Every field of a stationary kernel depends on the pair (i, j) only
+// through d = |x_i - x_j| (kernel_matrix.py:119-151), and on a collocation grid
+// (linspace(0,1,N)*scale, model_GP_solver_2d.py:369-374) the n^2 pairs take only ~5n distinct
+// fp64 values of d: each diagonal k = i - j holds a handful of rounding variants of k*h.  The
+// host (gpk_create) groups the pairs of each axis by the EXACT value of d, per diagonal: class
+// (k, v), k in [0, n), v < nvar(k) <= CLS_VMAX, ids [cbase[k], cbase[k+1]).  The fields are then
+// evaluated once per class (bitwise the per-pair values: same d, same code) and the
+// hyper-parameter contraction sum_ij G[i,j] f(d_ij) becomes sum_c (sum_{ij in c} G[i,j]) f(d_c).
+// Grids whose diagonals carry more than CLS_VMAX distinct distances use the per-pair kernels.
+constexpr int CLS_VMAX = 32;
+struct ClassArgs {
+  int ncls;              // classes of this axis (0: per-pair path)
+  int vmax;              // max variants per diagonal (<= CLS_VMAX)
+  const double* dist;    // [ncls] d of each class
+  const int* cid;        // [p*p] class of pair (i, j); -1 on pads
+  const int* cbase;      // [n+1] first class of diagonal k
+  double* kval;          // [ncls] kappa(d)      (+ jitter is added per element)
+  double* dval;          // [ncls] d2k or |dk| (the D_x1 sign s_ij is applied per element)
+  // hyper-parameter contraction: row chunk c of the class-sum launch writes its partial sums
+  // of G_K[i,j] and s_ij G_D[i,j] over every class to part[c][.] / part[nchunk + c][.]; the
+  // contraction launch adds the nchunk partials of each class in chunk order
+  int nchunk, rb;        // row chunks of rb rows
+  double* part;          // [2][nchunk][ncls]
+};
+
 struct AssembleArgs {
   const double* x;       // coords [n] (padded buffer ok)
   int n;                 // true size
@@ -115,9 +140,11 @@ struct AssembleArgs {
   // (nullable piv: not fused).  Same outputs as the sweep's pivot_init.
   double* piv; double* ldet; double* pst; int* status;
   unsigned int* flag;    // zero-initialised counter (re-armed by the pivot workgroup)
+  ClassArgs cls;         // ncls > 0: class evaluation + gather instead of per-pair evaluation
 };
+// eval_only (class path): the class values (+ prep) only, no gather / pivot-0 launch
 hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, const PrepArgs& prep,
-                           hipStream_t s);
+                           hipStream_t s, bool eval_only = false);
 hipError_t launch_pairs(int kind, int q, const double* x1, const double* x2, long n,
                         const AxisConst* kc, int deriv, double* out, hipStream_t s);
 hipError_t launch_cross(int kind, int q, const double* xr, int nr, const double* xc, int nc,
@@ -141,6 +168,20 @@ struct SpdArgs {
 hipError_t launch_spd_inverse(SpdArgs* args, int nmat, double** final_out, hipStream_t s,
                               bool pivot0_done = false);
 hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
+
+// Persistent ("chain") form of the small-factor inverse (spdinv.hip): every sweep in one launch,
+// ordered by flags; K^{-1} ends in X.  Gather mode (cid != nullptr) builds K from the distance
+// classes first and writes Kc and D on the way (no assembly launch); otherwise X holds K.
+constexpr int CHAIN_MAX_BLOCKS = 256;
+struct ChainArgs {
+  double* X; double* PB; double* piv; double* ldet; double* pst; int* status;
+  unsigned int* flags;  // [T*T + T + 1], zero-initialised
+  int p, n;
+  const int* cid; const double* kval; const double* dval; const double* x; double jitter;
+  double* Kc; double* D;
+};
+bool spd_chain_ok(const int* p, int nmat);
+hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s);
 
 // Large-factor path (spdinv_big.hip): 64-wide pivots, panel + lower-tile MFMA update per sweep,
 // next pivot factored inside the update launch.  In place: K^{-1} ends in X.  Y is used as the
@@ -237,6 +278,7 @@ struct PGradArgs {
   double halfc;                           // 1D mode: 0.5*logdet flag
   int deriv;
   double* part;                           // [nblocks * 3*QMAX]
+  ClassArgs cls;                          // ncls > 0: class sums + per-class contraction
 };
 struct TailArgs;  // stepk.h
 // tail (nullable): the fused step tail carried by the same launch (stepk.h TailArgs)
@@ -244,5 +286,6 @@ hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int nax
                         int blocks_per_axis, const StepScalars* sc, hipStream_t s,
                         const TailArgs* tail = nullptr, int shard_rank = 0, int shard_n = 1);
 int pgrad_blocks(int n);
+int pgrad_class_blocks(int ncls);  // contraction blocks of the class path
 
 }  // namespace gpk

@@ -1,0 +1,68 @@
+// gpk_trace.h — device-side timeline probes for latency tuning (build: `make trace`, which
+// defines GPK_TRACE and writes libgpk_trace.so; the product build compiles them away).
+//
+// Every translation unit owns two slot arrays (first arrival / last departure, read from the
+// 100 MHz constant clock, s_memrealtime) and exposes them to gpk_api.cpp through
+// trace_fetch_<tu> / trace_reset_<tu>.  Slots are global across TUs (see SLOT_* below), so
+// one step's timeline is the union of all TUs' arrays.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gpk {
+
+constexpr int TRACE_SLOTS = 64;
+enum TraceSlot {
+  SLOT_CLASS_EVAL = 0, SLOT_GATHER = 1, SLOT_PIVOT0_WAIT = 2, SLOT_PIVOT0 = 3,
+  SLOT_SWEEP = 4,         // + k (k < 16): whole sweep launch k
+  SLOT_SWEEP_PIVOT = 20,  // + k: the next-pivot factorisation inside sweep k
+  SLOT_CLASS_SUM = 40, SLOT_PGRAD = 41, SLOT_PG_CONTRACT = 42, SLOT_PG_GROUP = 43,
+  SLOT_PG_TOP = 44, SLOT_PG_UPLANE = 45, SLOT_PG_FINAL = 46,
+  // dispatch spread (last workgroup start) and intermediate points
+  SLOT_PG_START = 47, SLOT_PG_STAGED = 48, SLOT_CSUM_START = 49, SLOT_CEVAL_START = 50,
+  SLOT_GATHER_START = 51, SLOT_CSUM_LOADED = 52,
+};
+
+#ifdef GPK_TRACE
+#define GPK_TRACE_TU(tu)                                                                  \
+  namespace {                                                                             \
+  __device__ unsigned long long trace_lo[TRACE_SLOTS], trace_hi[TRACE_SLOTS];             \
+  }                                                                                       \
+  void trace_fetch_##tu(uint64_t* lo, uint64_t* hi) {                                     \
+    (void)hipMemcpyFromSymbol(lo, HIP_SYMBOL(trace_lo), sizeof(trace_lo));                \
+    (void)hipMemcpyFromSymbol(hi, HIP_SYMBOL(trace_hi), sizeof(trace_hi));                \
+  }                                                                                       \
+  void trace_reset_##tu() {                                                               \
+    unsigned long long lo[TRACE_SLOTS], hi[TRACE_SLOTS];                                  \
+    for (int i = 0; i < TRACE_SLOTS; ++i) lo[i] = ~0ull, hi[i] = 0ull;                    \
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(trace_lo), lo, sizeof(lo));                        \
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(trace_hi), hi, sizeof(hi));                        \
+  }
+// probes fire in thread 0 of ONE workgroup per slot (a first-block / last-block / critical
+// block); same-address atomics from every workgroup would serialise and distort the timeline
+#define TR_FIRST (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+#define TR_LAST                                                                       \
+  (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1 && blockIdx.y == gridDim.y - 1 && \
+   blockIdx.z == gridDim.z - 1)
+#define TR_LO(slot) atomicMin(&trace_lo[slot], (unsigned long long)wall_clock64())
+#define TR_HI(slot) atomicMax(&trace_hi[slot], (unsigned long long)wall_clock64())
+#else
+#define GPK_TRACE_TU(tu)                                   \
+  void trace_fetch_##tu(uint64_t* lo, uint64_t* hi) {      \
+    for (int i = 0; i < TRACE_SLOTS; ++i) lo[i] = hi[i] = 0; \
+  }                                                        \
+  void trace_reset_##tu() {}
+#define TR_FIRST false
+#define TR_LAST false
+#define TR_LO(slot) ((void)0)
+#define TR_HI(slot) ((void)0)
+#endif
+
+void trace_fetch_assemble(uint64_t* lo, uint64_t* hi);
+void trace_reset_assemble();
+void trace_fetch_spdinv(uint64_t* lo, uint64_t* hi);
+void trace_reset_spdinv();
+void trace_fetch_pgrad(uint64_t* lo, uint64_t* hi);
+void trace_reset_pgrad();
+
+}  // namespace gpk

@@ -15,14 +15,19 @@
 // 2D mode reads materialised G_K / G_D tiles; 1D mode forms them on the fly from K^{-1} and
 // the vectors alpha = K^{-1}u, beta = K^{-1}D^T R, R (model_GP_solver_1d.py:80-149):
 //   G_K = c/2 K^{-1} - 1/2 alpha alpha^T - v beta alpha^T,   G_D = v R alpha^T.
+#include <algorithm>
+
 #include "gpk_internal.h"
 #include "stepk_dev.h"
+#include "gpk_trace.h"
 
 #ifndef GPK_PG_PAIRS
 #define GPK_PG_PAIRS 64
 #endif
 
 namespace gpk {
+
+GPK_TRACE_TU(pgrad)
 
 constexpr int PAIRS = GPK_PG_PAIRS;  // pairs per workgroup (PAIRS/32 rows x 32 cols of a 32x32 tile)
 constexpr int PG_SUB = 1024 / PAIRS;  // workgroups per tile
@@ -40,8 +45,9 @@ struct PGradBatch {
 // sums the group partials (group order) into pg and runs finalize_body.  Cross-XCD hand-off per
 // MI355X_MICROARCH.md §inter-workgroup visibility: producers store write-through (sc1), every
 // storing wave drains (vmcnt 0), a barrier, then ONE lane's agent-scope ticket add; the block
-// whose add came last does one agent acquire (+ vmcnt 0 + barrier) before reading.  No
-// __threadfence() per block (its L2 write-back made this tail 4x slower).  Counters are
+// whose add came last (told by the value its add returned) reads every handed-off byte with sc1
+// loads after a barrier -- the guide's sc1 row, no agent acquire (~1.7 us per level saved).
+// No __threadfence() per block (its L2 write-back made this tail 4x slower).  Counters are
 // re-armed by the blocks that consume them.
 __device__ __forceinline__ void st_wt(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store sc1
@@ -52,29 +58,28 @@ __device__ __forceinline__ bool arrive_last(unsigned int* counter, unsigned int 
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned prev = atomicAdd(counter, 1u);
-    const bool last = prev == n - 1u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *s_flag = last;
+    *s_flag = prev == n - 1u;
   }
   __syncthreads();
   return *s_flag != 0;
 }
 
-// sum_{k<n} p[k*stride] in index order, 16 loads in flight per batch (latency-bound chain)
+__device__ __forceinline__ double ld_wt(const double* p) {  // global_load sc1 (L2-served)
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum_{k<n} p[k*stride] in index order (sc1 loads), 16 in flight per batch (latency-bound chain)
 __device__ __forceinline__ double strided_sum(const double* p, int stride, int n) {
   double acc = 0.0;
   int k = 0;
   for (; k + 16 <= n; k += 16) {
     double v[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = p[(size_t)(k + j) * stride];
+    for (int j = 0; j < 16; ++j) v[j] = ld_wt(p + (size_t)(k + j) * stride);
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc += v[j];
   }
-  for (; k < n; ++k) acc += p[(size_t)k * stride];
+  for (; k < n; ++k) acc += ld_wt(p + (size_t)k * stride);
   return acc;
 }
 
@@ -84,6 +89,8 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
   const int t = threadIdx.x;
   const int gi = blk / T.tg;
   const int gsize = min(T.tg, b.bpa - gi * T.tg);
+  if (t == 0 && blk == 0 && axis == 0) TR_HI(SLOT_PG_CONTRACT);
+  if (t == 0 && blk == b.bpa - 1 && axis == b.naxes - 1) TR_HI(SLOT_PG_START);
   if (!arrive_last(T.gcount + axis * T.ngpa + gi, (unsigned)gsize, &s_last)) return;
   const double* part = b.ax[axis].part;
   for (int x = t; x < 3 * QMAX; x += 256) {
@@ -93,7 +100,9 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
     st_wt(T.gpart + (size_t)(axis * T.ngpa + gi) * (3 * QMAX) + x, acc);
   }
   if (t == 0) T.gcount[axis * T.ngpa + gi] = 0u;  // re-arm (no other user this step)
+  if (t == 0) TR_HI(SLOT_PG_GROUP);
   if (!arrive_last(T.top, (unsigned)(b.naxes * T.ngpa), &s_last)) return;
+  if (t == 0) TR_LO(SLOT_PG_TOP);
   for (int e = t; e < b.naxes * 3 * QMAX; e += 256) {
     const int ax = e / (3 * QMAX), x = e % (3 * QMAX);
     double acc = 0.0;
@@ -102,32 +111,134 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
   }
   __syncthreads();  // pg (global) written by this block is visible to it after the barrier
   if (t == 0) *T.top = 0u;
+  if (t == 0) TR_HI(SLOT_PG_TOP);
   finalize_body(T.fin);
+  if (t == 0) TR_HI(SLOT_PG_FINAL);
 }
 
-template <bool MATERN, bool COS, int DERIV, bool MODE1D>
+// ---- class path (gpk_internal.h ClassArgs) -------------------------------------------------
+// Class sums over one row chunk: part[c][u] = sum_{(i,j) in u, i in chunk c} G_K[i,j] (and
+// s_ij G_D[i,j] in the second half).  Workgroup (chunk c, band of 64 diagonals); lane = diagonal
+// k.  At row r lane k reads the lower pair (r, r-k) and the upper pair (r, r+k): contiguous row
+// segments across the wave (coalesced), and every ordered pair is read exactly once over the
+// grid.  The 4 waves take interleaved rows, load 4 rows' operands before accumulating (memory-
+// level parallelism), and keep V running sums per lane (one per distance variant of the lane's
+// diagonal, selected branch-free); they add them into LDS in wave order: deterministic.
+template <int V, int DERIV, bool MODE1D>
+__global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
+                                                       const StepScalars* __restrict__ sc) {
+  const int axis = blockIdx.z, band = blockIdx.y, chunk = blockIdx.x;
+  const PGradArgs& A = b.ax[axis];
+  const ClassArgs& C = A.cls;
+  const int n = A.n, p = A.p;
+  if (band * 64 >= n || chunk >= C.nchunk) return;  // shorter axis
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (TR_FIRST) TR_LO(SLOT_CLASS_SUM);
+  if (TR_LAST) TR_LO(SLOT_CSUM_START);
+  const int k = band * 64 + lane;
+  const bool kv = k < n;
+  const int cb = kv ? C.cbase[k] : 0;
+  const int r0 = chunk * C.rb, r1 = min(n, r0 + C.rb);
+  double ak[V], ad[V];
+#pragma unroll
+  for (int x = 0; x < V; ++x) ak[x] = ad[x] = 0.0;
+  double vs = 0.0, hc = 0.0;
+  if (MODE1D) {
+    vs = sc->v;
+    hc = A.halfc;
+  }
+  // operands of the ordered pair (i, j); ok = false: v = -1 (matches no variant).  Branch-free:
+  // out-of-range pairs load the clamped element (0, 0), so all loads of a 4-row group issue
+  // back to back instead of behind per-branch waits.
+  auto load = [&](bool ok, int i, int j, int& v, double& gk, double& gd) {
+    i = ok ? i : 0;
+    j = ok ? j : 0;
+    const size_t o = (size_t)i * p + j;
+    v = ok ? C.cid[o] - cb : -1;
+    if (MODE1D) {  // G_K = c/2 K^{-1} - 1/2 alpha alpha^T - v beta alpha^T, G_D = v R alpha^T
+      const double ai = A.alpha[i], aj = A.alpha[j];
+      gk = hc * A.Kinv[o] - 0.5 * ai * aj - vs * A.beta[i] * aj;
+      gd = vs * A.R[i] * aj;
+    } else {
+      gk = A.GK[o];
+      gd = A.GD[o];
+    }
+    if (DERIV == 1 && !(A.x[i] - A.x[j] >= 0.0)) gd = -gd;
+  };
+  for (int base = r0; base < r1; base += 16) {
+    int vl[4], vu[4];
+    double kl[4], dl[4], ku[4], du[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int r = base + w + 4 * s;
+      const bool in = kv && r < r1;
+      load(in && r >= k, r, r - k, vl[s], kl[s], dl[s]);
+      load(in && k > 0 && r + k < n, r, r + k, vu[s], ku[s], du[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int x = 0; x < V; ++x) {
+        ak[x] += (vl[s] == x) ? kl[s] : 0.0;
+        ad[x] += (vl[s] == x) ? dl[s] : 0.0;
+        ak[x] += (vu[s] == x) ? ku[s] : 0.0;
+        ad[x] += (vu[s] == x) ? du[s] : 0.0;
+      }
+  }
+  if (TR_FIRST) TR_HI(SLOT_CSUM_LOADED);
+  __shared__ double red[2][V][64];
+#pragma unroll
+  for (int ww = 0; ww < 4; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int x = 0; x < V; ++x) {
+        red[0][x][lane] = ww == 0 ? ak[x] : red[0][x][lane] + ak[x];
+        red[1][x][lane] = ww == 0 ? ad[x] : red[1][x][lane] + ad[x];
+      }
+    }
+    __syncthreads();
+  }
+  double* pk = C.part + (size_t)chunk * C.ncls;
+  double* pd = C.part + (size_t)(C.nchunk + chunk) * C.ncls;
+  for (int e = t; e < 64 * V; e += 256) {
+    const int l = e & 63, x = e >> 6, kk = band * 64 + l;
+    if (kk < n && x < C.cbase[kk + 1] - C.cbase[kk]) {
+      pk[C.cbase[kk] + x] = red[0][x][l];
+      pd[C.cbase[kk] + x] = red[1][x][l];
+    }
+  }
+  if (TR_FIRST) TR_HI(SLOT_CLASS_SUM);
+  if (TR_LAST) TR_HI(SLOT_CSUM_START);
+}
+
+constexpr int PG_CLS = 16;  // classes per contraction workgroup
+
+template <bool MATERN, bool COS, int DERIV, bool MODE1D, bool CLS>
 __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
                                                     const StepScalars* __restrict__ sc) {
   const int axis = blockIdx.y;
   const int blk = blockIdx.x;
-  if (axis == b.naxes) {  // fused tail: dL/dU + Adam on U (grid-stride over the solution grid)
+  if (TR_FIRST) TR_LO(SLOT_PGRAD);
+  if (axis == b.naxes) {
+    if (threadIdx.x == 0 && blk == 0) TR_LO(SLOT_PG_UPLANE);  // fused tail: dL/dU + Adam on U (grid-stride over the solution grid)
     const int nu = tail_nu(b.tail.adam.L);
     for (int e = blk * 256 + threadIdx.x; e < nu; e += gridDim.x * 256) adam_u_elem(b.tail.adam, e);
+    if (threadIdx.x == 0 && blk == 0) TR_HI(SLOT_PG_UPLANE);
     return;
   }
+  if (blk >= b.bpa) return;  // the U plane is wider than the gradient planes
+  const bool trl = threadIdx.x == 0 && blk == b.bpa - 1 && axis == b.naxes - 1;
+  if (trl) TR_LO(SLOT_PG_START);
   const PGradArgs& A = b.ax[axis];
-  const int tile = blk / PG_SUB, chunk = blk % PG_SUB;
-  if (tile >= b.tiles[axis]) {  // no pairs here (shorter axis); its partial slot stays zero
+  const int tile = CLS ? blk : blk / PG_SUB, chunk = blk % PG_SUB;
+  if (CLS ? blk * PG_CLS >= A.cls.ncls : tile >= b.tiles[axis]) {
+    // no pairs / classes here (shorter axis); its partial slot stays zero
     if (b.tail.fused) pgrad_tail(b, axis, blk, q);
     return;
   }
   // sharded step (never fused): another rank's pair tile -- this slot is never written, so it
   // stays zero and the cross-rank all-reduce of the reduced partials counts each tile once
   if (b.shard_n > 1 && tile % b.shard_n != b.shard_rank) return;
-  int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-  while ((I + 1) * (I + 2) / 2 <= tile) ++I;
-  while (I * (I + 1) / 2 > tile) --I;
-  const int J = tile - I * (I + 1) / 2;
 
   __shared__ double sd[PAIRS], swk[PAIRS], swd[PAIRS];
   __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
@@ -138,7 +249,37 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
     sa[t] = A.kc->a[t];
     so[t] = A.kc->om[t];
   }
-  if (t < PAIRS) {  // stage pair t
+  constexpr int NP = CLS ? PG_CLS : PAIRS;  // staged (d, w_K, w_D) entries
+  if (CLS) {  // class blk * PG_CLS + (t & 15): weights = its chunk partials, added in chunk order
+    const ClassArgs& C = A.cls;
+    const int ul = t & (PG_CLS - 1), cs = t / PG_CLS;  // 16 chunk slices
+    const int u = blk * PG_CLS + ul;
+    double sk = 0.0, sdd = 0.0;
+    if (u < C.ncls)
+      for (int c = cs; c < C.nchunk; c += 256 / PG_CLS) {
+        sk += C.part[(size_t)c * C.ncls + u];
+        sdd += C.part[(size_t)(C.nchunk + c) * C.ncls + u];
+      }
+    sacc[cs >> 1][0][(cs & 1) * PG_CLS + ul] = sk;  // scratch: [16 slices][16 classes] x 2
+    sacc[cs >> 1][1][(cs & 1) * PG_CLS + ul] = sdd;
+    __syncthreads();
+    if (t < PG_CLS) {
+      double a = 0.0, d = 0.0;
+#pragma unroll
+      for (int x = 0; x < 256 / PG_CLS; ++x) {
+        a += sacc[x >> 1][0][(x & 1) * PG_CLS + t];
+        d += sacc[x >> 1][1][(x & 1) * PG_CLS + t];
+      }
+      const bool ok = u < C.ncls;
+      sd[t] = ok ? C.dist[u] : 0.0;
+      swk[t] = ok ? a : 0.0;
+      swd[t] = ok ? d : 0.0;
+    }
+  } else if (t < PAIRS) {  // stage pair t
+    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+    while (I * (I + 1) / 2 > tile) --I;
+    const int J = tile - I * (I + 1) / 2;
     const int i = I * 32 + chunk * (PAIRS / 32) + (t >> 5), j = J * 32 + (t & 31);
     double d = 0.0, wk = 0.0, wd = 0.0;
     if (i < A.n && j < A.n) {
@@ -177,6 +318,7 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
     swd[t] = wd;
   }
   __syncthreads();
+  if (TR_FIRST) TR_HI(SLOT_PG_STAGED);
 
   const int g = t >> 5, ql = t & 31;
   double* out = A.part + (size_t)blk * (3 * QMAX);
@@ -185,7 +327,7 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
     double accf = 0.0, accl = 0.0, accw = 0.0;
     if (c < q) {
       const double a = sa[c], om = so[c];
-      for (int e = g; e < PAIRS; e += 8) {
+      for (int e = g; e < NP; e += 8) {
         const double wk = swk[e], wd = swd[e];
         if (wk == 0.0 && wd == 0.0) continue;
         const double d = sd[e];
@@ -243,16 +385,51 @@ int pgrad_blocks(int n) {
   return T * (T + 1) / 2 * PG_SUB;
 }
 
+int pgrad_class_blocks(int ncls) { return (ncls + PG_CLS - 1) / PG_CLS; }
+
+template <int V>
+static void launch_csum_v(const PGradBatch& b, int nchunk, int nbands, int deriv, int mode1d,
+                          const StepScalars* sc, hipStream_t s) {
+  dim3 grid(nchunk, nbands, b.naxes);
+  if (mode1d)
+    hipLaunchKernelGGL((class_sum_kernel<V, 2, true>), grid, dim3(256), 0, s, b, sc);
+  else if (deriv == 2)
+    hipLaunchKernelGGL((class_sum_kernel<V, 2, false>), grid, dim3(256), 0, s, b, sc);
+  else
+    hipLaunchKernelGGL((class_sum_kernel<V, 1, false>), grid, dim3(256), 0, s, b, sc);
+}
+
+template <bool MATERN, bool COS, bool CLS>
+static void launch_pg_c(const PGradBatch& b, int naxes, int bpa, int q, int deriv, int mode1d,
+                        const StepScalars* sc, hipStream_t s) {
+  // the U plane (dL/dU + Adam) gets one element per thread when it is wider than bpa blocks
+  const int ublocks = b.tail.fused ? (tail_nu(b.tail.adam.L) + 255) / 256 : 0;
+  dim3 grid(std::max(bpa, std::min(ublocks, 4096)), naxes + (b.tail.fused ? 1 : 0));
+  if (mode1d) {
+    hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, true, CLS>), grid, dim3(256), 0, s, b, q, sc);
+  } else if (deriv == 2) {
+    hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, false, CLS>), grid, dim3(256), 0, s, b, q, sc);
+  } else {
+    hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 1, false, CLS>), grid, dim3(256), 0, s, b, q, sc);
+  }
+}
+
 template <bool MATERN, bool COS>
 static void launch_pg_t(const PGradBatch& b, int naxes, int bpa, int q, int deriv, int mode1d,
                         const StepScalars* sc, hipStream_t s) {
-  dim3 grid(bpa, naxes + (b.tail.fused ? 1 : 0));
-  if (mode1d) {
-    hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, true>), grid, dim3(256), 0, s, b, q, sc);
-  } else if (deriv == 2) {
-    hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, false>), grid, dim3(256), 0, s, b, q, sc);
+  if (b.ax[0].cls.ncls > 0) {
+    int nbands = 0, vmax = 0, nchunk = 0;
+    for (int k = 0; k < naxes; ++k) {
+      nbands = std::max(nbands, (b.ax[k].n + 63) / 64);
+      vmax = std::max(vmax, b.ax[k].cls.vmax);
+      nchunk = std::max(nchunk, b.ax[k].cls.nchunk);
+    }
+    if (vmax <= 8) launch_csum_v<8>(b, nchunk, nbands, deriv, mode1d, sc, s);
+    else if (vmax <= 16) launch_csum_v<16>(b, nchunk, nbands, deriv, mode1d, sc, s);
+    else launch_csum_v<32>(b, nchunk, nbands, deriv, mode1d, sc, s);
+    launch_pg_c<MATERN, COS, true>(b, naxes, bpa, q, deriv, mode1d, sc, s);
   } else {
-    hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 1, false>), grid, dim3(256), 0, s, b, q, sc);
+    launch_pg_c<MATERN, COS, false>(b, naxes, bpa, q, deriv, mode1d, sc, s);
   }
 }
 
@@ -267,6 +444,7 @@ hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int nax
     b.ax[k] = a[k];
     int T = a[k].p / 32;
     b.tiles[k] = T * (T + 1) / 2;
+    if ((a[k].cls.ncls > 0) != (a[0].cls.ncls > 0) || a[k].cls.vmax > CLS_VMAX) return hipErrorInvalidValue;
   }
   b.naxes = naxes;
   b.bpa = blocks_per_axis;

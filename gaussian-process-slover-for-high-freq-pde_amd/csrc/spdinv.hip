@@ -21,10 +21,15 @@
 // recomputes the two 32x32 panel pieces it needs; the workgroup that produces the NEXT
 // pivot tile factors it in its tail, so the next launch finds L^{-1} ready: N/32 launches,
 // batched over both Kronecker factors.
+#include <algorithm>
+
 #include "gpk_internal.h"
 #include "spd_pivot.h"
+#include "gpk_trace.h"
 
 namespace gpk {
+
+GPK_TRACE_TU(spdinv)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -81,14 +86,20 @@ __device__ __forceinline__ void store_quad(double* s, int ld, int wr, int wc, in
 }
 
 __global__ __launch_bounds__(256) void sweep_kernel(SpdBatch b, int k) {
-  const int m = blockIdx.y;
+  // grid (nmat, tiles): the factors are interleaved in dispatch order, and tile numbering starts
+  // at the tile that factors the next pivot (the critical path of the launch): it is dispatched
+  // first instead of after up to 2 T^2 other workgroups
+  const int m = blockIdx.x;
   const int p = b.p[m];
   const int T = b.T[m];
   if (k >= T) return;  // this factor is already inverted
   const int last = (k == T - 1);
-  const int tile = blockIdx.x;
-  if (tile >= T * T) return;
+  if ((int)blockIdx.y >= T * T) return;
+  const int tile = (int)(blockIdx.y + (last ? 0 : (k + 1) * (T + 1))) % (T * T);
   const int I = tile / T, J = tile % T;
+  // probes: the block that factors the next pivot (tile (0,0) of factor 0 in the last sweep)
+  const bool trb = threadIdx.x == 0 && m == 0 && k < 16 && blockIdx.y == 0;
+  if (trb) TR_LO(SLOT_SWEEP + k);
   const double* X = (k & 1) ? b.Y[m] : b.X[m];
   double* Y = (k & 1) ? b.X[m] : b.Y[m];
   const double* Li = b.piv[m] + (size_t)k * 1024;  // L^{-1} of pivot block k
@@ -163,14 +174,270 @@ __global__ __launch_bounds__(256) void sweep_kernel(SpdBatch b, int k) {
       atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
                 (unsigned long long)__double_as_longlong(mx));
     }
+    if (trb) TR_HI(SLOT_SWEEP + k);
     return;
   }
-  if (!nextpiv) return;  // block-uniform
+  if (!nextpiv) {  // block-uniform
+    if (trb) TR_HI(SLOT_SWEEP + k);
+    return;
+  }
   __syncthreads();
+  if (trb) TR_LO(SLOT_SWEEP_PIVOT + k);
   const double ls = pivot_chol_inv_block(sP, sM, pv, t, b.status[m]);
   double* piv = b.piv[m] + (size_t)(k + 1) * 1024;
   for (int e = t; e < 1024; e += 256) piv[e] = sM[(e >> 5) * SP + (e & 31)];
   if (t == 0) b.ldet[m][k + 1] = ls;
+  if (trb) TR_HI(SLOT_SWEEP_PIVOT + k);
+  if (trb) TR_HI(SLOT_SWEEP + k);
+}
+
+// ---- persistent dataflow form ("chain"): every sweep in ONE launch ------------------------
+// The sweep above pays a launch boundary per pivot block: the pivot workgroup's pre-pivot work
+// (~4 us of loads + two MFMA passes) plus the inter-kernel gap (~1.7 us) on top of the 5.4-us
+// factorisation, 8 times at 256^2 (tools/timeline.py).  Here one workgroup per tile owns its
+// tile for the whole inverse (in MFMA accumulators) and sweeps are ordered by flags:
+//   * tile (I, J) is read by other workgroups only as the panel of sweep I; its owner publishes
+//     it once, after sweep I-1, into the panel buffer PB (write-once, no ping-pong hazard);
+//   * L^{-1} of pivot k is published once into piv[k] by the owner of (k, k);
+//   * hand-offs follow MI355X_MICROARCH.md's sc1 row: payload stored sc1 by every wave, each
+//     wave's vmcnt(0), a barrier, one lane's sc1 flag store; the consumer polls the flag with an
+//     sc1 load, a barrier, then sc1 loads of the payload.
+// The per-sweep critical path is the pivot owner's hop (poll + loads + two MFMA passes) plus its
+// factorisation.  All workgroups wait on one another, so the grid must be co-resident: used
+// when sum_m T_m^2 <= CHAIN_MAX_BLOCKS (one workgroup per CU at most).  The arithmetic is the
+// sweep kernel's operation for operation: the results are bitwise equal.
+struct ChainFactor {
+  double* X;            // in: assembled K (read mode); out: K^{-1}
+  double* PB;           // panel buffer [p*p]: tile (I, J) as it is after sweep I-1
+  double* piv;          // [T][32*32] L^{-1} of each pivot block
+  double* ldet;         // [T]
+  double* pst;          // refinement gate [2]
+  int* status;
+  unsigned int* flags;  // [T*T] panel ready, [T] pivot ready, [1] done counter (zero; re-armed)
+  int p, n, T;
+  // gather mode: K from the distance classes (+ jitter), kept copy Kc and D written on the way
+  const int* cid; const double* kval; const double* dval; const double* x; double jitter;
+  double* Kc; double* D;
+};
+struct ChainBatch {
+  ChainFactor f[2];
+};
+
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_flag(unsigned int* f) {
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    __builtin_amdgcn_s_sleep(1);
+}
+// every wave drained its sc1 stores -> barrier -> one lane raises the flag
+__device__ __forceinline__ void signal_flag(unsigned int* f) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int DERIV, bool GATHER>
+__global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
+  const int m = blockIdx.y;
+  const ChainFactor& F = b.f[m];
+  const int T = F.T, p = F.p;
+  const int tile = blockIdx.x;
+  if (tile >= T * T) return;
+  const int I = tile / T, J = tile % T;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int tx = t & 31, ty = t >> 5;
+  unsigned int* panel_rdy = F.flags;
+  unsigned int* piv_rdy = F.flags + T * T;
+  unsigned int* done = F.flags + T * T + T;
+  __shared__ double sL[32 * SA];
+  __shared__ double sXI[32 * SB], sXJ[32 * SB];
+  __shared__ double sP[32 * SP], sM[32 * SP], pv[32];
+  __shared__ unsigned int s_last;
+
+  // own tile, this wave's quadrant: rows 16 wr + (lane >> 4) + 4 r, column 16 wc + (lane & 15)
+  d4 acc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = I * 32 + 16 * wr + (lane >> 4) + 4 * r, j = J * 32 + 16 * wc + (lane & 15);
+    const size_t o = (size_t)i * p + j;
+    if (GATHER) {
+      const int u = F.cid[o];
+      double kv, dv;
+      if (u >= 0) {
+        kv = F.kval[u];
+        if (i == j) kv += F.jitter;
+        dv = F.dval[u];
+        if (DERIV == 1 && !(F.x[i] - F.x[j] >= 0.0)) dv = -dv;  // JAX abs'(0) = +1
+      } else {
+        kv = (i == j) ? 1.0 : 0.0;
+        dv = 0.0;
+      }
+      if (F.Kc) F.Kc[o] = kv;
+      if (DERIV) F.D[o] = dv;
+      acc[r] = kv;
+    } else {
+      acc[r] = F.X[o];
+    }
+  }
+  auto publish_tile = [&](void) {  // PB tile (I, J) <- acc, then its flag
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      st_sc1(F.PB + (size_t)(I * 32 + 16 * wr + (lane >> 4) + 4 * r) * p + J * 32 + 16 * wc + (lane & 15),
+             acc[r]);
+    signal_flag(panel_rdy + I * T + J);
+  };
+  const bool trm = t == 0 && m == 0;  // probes (gpk_trace.h): factor 0's pivot owners
+  auto factor_pivot = [&](int kp, bool with_tile) {  // acc: Schur complement of pivot block kp
+    store_quad(sP, SP, wr, wc, lane, acc);
+    __syncthreads();
+    if (with_tile) {  // this tile as the panel of sweep kp (its stores drain with the pivot's)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        st_sc1(F.PB + (size_t)(I * 32 + 16 * wr + (lane >> 4) + 4 * r) * p + J * 32 + 16 * wc + (lane & 15),
+               acc[r]);
+    }
+    if (trm && kp > 0 && kp < 17) TR_LO(SLOT_SWEEP_PIVOT + kp - 1);
+    if (trm && kp == 0) TR_LO(SLOT_PIVOT0);
+    const double ls = pivot_chol_inv_block(sP, sM, pv, t, F.status);
+    for (int e = t; e < 1024; e += 256) st_sc1(F.piv + (size_t)kp * 1024 + e, sM[(e >> 5) * SP + (e & 31)]);
+    if (t == 0) F.ldet[kp] = ls;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      if (with_tile) __hip_atomic_store(panel_rdy + I * T + J, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(piv_rdy + kp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP_PIVOT + kp - 1);
+    if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP + kp - 1);
+    if (trm && kp == 0) TR_HI(SLOT_PIVOT0);
+  };
+  if (trm && tile == 0) TR_LO(SLOT_GATHER);
+  if (I == 0 && J == 0) {
+    if (t == 0) {
+      F.pst[0] = acc[0];  // K_00 = max diag K (stationary kernel + jitter): refinement gate
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(F.pst + 1), 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);  // max diag K^{-1}, atomicMax'd at the end
+    }
+  }
+  if (I == 0 && J == 0) factor_pivot(0, true);  // row 0 is the panel of sweep 0
+  else if (I == 0) publish_tile();
+
+  for (int k = 0; k < T; ++k) {
+    const bool needI = I != k, needJ = J != k && J != I;
+    // the panel tiles are usually published long before the pivot: fetch them first, then
+    // wait for L^{-1}_k
+    if (t == 0) {
+      if (needI) wait_flag(panel_rdy + k * T + I);
+      if (needJ) wait_flag(panel_rdy + k * T + J);
+    }
+    __syncthreads();
+    double xi[4], xj[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = ty + 8 * r;
+      xi[r] = needI ? ld_sc1(F.PB + (size_t)(k * 32 + row) * p + I * 32 + tx) : 0.0;
+      xj[r] = needJ ? ld_sc1(F.PB + (size_t)(k * 32 + row) * p + J * 32 + tx) : 0.0;
+    }
+    if (t == 0) {
+      wait_flag(piv_rdy + k);
+      if (trm && I == k + 1 && J == k + 1 && k < 16) TR_LO(SLOT_SWEEP + k);
+    }
+    __syncthreads();
+    const double* Li = F.piv + (size_t)k * 1024;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = ty + 8 * r;
+      sL[row * SA + tx] = ld_sc1(Li + row * 32 + tx);
+      if (needI) sXI[row * SB + tx] = xi[r];
+      if (needJ) sXJ[row * SB + tx] = xj[r];
+    }
+    __syncthreads();
+    const double* sVJ = (J == I) ? sXI : sXJ;
+    d4 vi = {0.0, 0.0, 0.0, 0.0}, vj = {0.0, 0.0, 0.0, 0.0};
+    if (needI) vi = mma_t(sL, SA, 1, sXI, SB, 1, wr, wc, lane, vi);
+    if (needJ) vj = mma_t(sL, SA, 1, sXJ, SB, 1, wr, wc, lane, vj);
+    __syncthreads();
+    if (needI) store_quad(sXI, SB, wr, wc, lane, vi);
+    if (needJ) store_quad(sXJ, SB, wr, wc, lane, vj);
+    __syncthreads();
+    d4 prod = {0.0, 0.0, 0.0, 0.0};
+    if (I == k && J == k) {
+      prod = mma_t(sL, 1, SA, sL, SA, 1, wr, wc, lane, prod);   // L^{-T} L^{-1}
+      acc = -prod;
+    } else if (I == k) {
+      acc = mma_t(sL, 1, SA, sVJ, SB, 1, wr, wc, lane, prod);  // L^{-T} V_J
+    } else if (J == k) {
+      acc = mma_t(sXI, 1, SB, sL, SA, 1, wr, wc, lane, prod);  // V_I^T L^{-1}
+    } else {
+      prod = mma_t(sXI, 1, SB, sVJ, SB, 1, wr, wc, lane, prod); // V_I^T V_J
+      acc = acc - prod;
+    }
+    if (k + 1 < T && I == k + 1 && J == k + 1) {
+      // the next pivot's owner: its panel tile is needed only with the pivot, so both are
+      // published behind one drain after the factorisation
+      factor_pivot(k + 1, true);
+    } else if (k + 1 < T && I == k + 1) {
+      publish_tile();  // panel of sweep k + 1
+    }
+    __syncthreads();  // LDS is refilled next sweep
+  }
+  // K^{-1} = -X after the last sweep
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
+    const double y = -acc[r];
+    F.X[(size_t)(I * 32 + row) * p + J * 32 + col] = y;
+    if (I == J && row == col) pv[row] = (I * 32 + row < F.n) ? y : 0.0;
+  }
+  __syncthreads();
+  if (I == J && t == 0) {  // refinement gate: max_i (K^{-1})_ii of this block
+    double mx = 0.0;
+    for (int j = 0; j < 32; ++j) mx = fmax(mx, pv[j]);
+    atomicMax(reinterpret_cast<unsigned long long*>(F.pst + 1), (unsigned long long)__double_as_longlong(mx));
+  }
+  if (trm && tile == 0) TR_HI(SLOT_GATHER);
+  // the last workgroup of this factor re-arms the flags for the next launch
+  if (t == 0) s_last = atomicAdd(done, 1u) == (unsigned)(T * T - 1);
+  __syncthreads();
+  if (s_last) {
+    for (int e = t; e < T * T + T; e += 256)
+      __hip_atomic_store(F.flags + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+bool spd_chain_ok(const int* p, int nmat) {
+  int blocks = 0;
+  for (int m = 0; m < nmat; ++m) blocks += (p[m] / 32) * (p[m] / 32);
+  return blocks <= CHAIN_MAX_BLOCKS;
+}
+
+hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s) {
+  ChainBatch b{};
+  int Tmax = 0;
+  bool gather = a[0].cid != nullptr;
+  for (int m = 0; m < nmat; ++m) {
+    ChainFactor& f = b.f[m];
+    f.X = a[m].X; f.PB = a[m].PB; f.piv = a[m].piv; f.ldet = a[m].ldet; f.pst = a[m].pst;
+    f.status = a[m].status; f.flags = a[m].flags; f.p = a[m].p; f.n = a[m].n; f.T = a[m].p / 32;
+    f.cid = a[m].cid; f.kval = a[m].kval; f.dval = a[m].dval; f.x = a[m].x; f.jitter = a[m].jitter;
+    f.Kc = a[m].Kc; f.D = a[m].D;
+    if ((a[m].cid != nullptr) != gather) return hipErrorInvalidValue;
+    Tmax = std::max(Tmax, f.T);
+  }
+  dim3 grid(Tmax * Tmax, nmat);
+  if (!gather)
+    hipLaunchKernelGGL((chain_kernel<0, false>), grid, dim3(256), 0, s, b);
+  else if (deriv == 1)
+    hipLaunchKernelGGL((chain_kernel<1, true>), grid, dim3(256), 0, s, b);
+  else
+    hipLaunchKernelGGL((chain_kernel<2, true>), grid, dim3(256), 0, s, b);
+  return hipGetLastError();
 }
 
 // One launch of the inverse: stage -1 = pivot_init, stage k >= 0 = sweep k (bench/profiling).
@@ -186,7 +453,7 @@ hipError_t launch_spd_stage(SpdArgs* a, int nmat, int stage, hipStream_t s) {
   if (stage < 0)
     hipLaunchKernelGGL(pivot_init_kernel, dim3(nmat), dim3(256), 0, s, b);
   else
-    hipLaunchKernelGGL(sweep_kernel, dim3(Tmax * Tmax, nmat), dim3(256), 0, s, b, stage);
+    hipLaunchKernelGGL(sweep_kernel, dim3(nmat, Tmax * Tmax), dim3(256), 0, s, b, stage);
   return hipGetLastError();
 }
 
@@ -210,7 +477,7 @@ hipError_t launch_spd_inverse(SpdArgs* a, int nmat, double** final_out, hipStrea
   }
   if (!pivot0_done) hipLaunchKernelGGL(pivot_init_kernel, dim3(nmat), dim3(256), 0, s, b);
   for (int k = 0; k < Tmax; ++k)
-    hipLaunchKernelGGL(sweep_kernel, dim3(Tmax * Tmax, nmat), dim3(256), 0, s, b, k);
+    hipLaunchKernelGGL(sweep_kernel, dim3(nmat, Tmax * Tmax), dim3(256), 0, s, b, k);
   return hipGetLastError();
 }
 

@@ -29,27 +29,67 @@ __device__ inline double block_sum(double v, double* sh) {
 }
 
 // Single-workgroup tail of the step: scalars, loss, small-parameter gradients + Adam.
+// Latency-bound (one workgroup on the step's critical path): every global load it needs is
+// issued up front (one memory round trip), and the small parameters' gradients and Adam updates
+// stay in the registers of the thread that owns them (no store / barrier / reload).
 __device__ inline void finalize_body(const FinalizeArgs& f) {
-  __shared__ double sh[4];
+  __shared__ double sh[4], sld[2], sg[2];
   const int t = threadIdx.x;
   const Layout& L = f.L;
-  double quad = 0.0, egap = 0.0, bgap = 0.0;
+  // ---- phase 0: loads
+  double quad = 0.0, egap = 0.0;
   for (int i = t; i < f.nquad; i += 256) quad += f.red_quad[i];
   for (int i = t; i < f.negap; i += 256) egap += f.red_egap[i];
-  quad = block_sum(quad, sh);
-  egap = block_sum(egap, sh);
-  bgap = *f.bgap;  // boundary gap of U at the start of the step (assembly launch)
-  if (t == 0 && f.viol)
-    for (int a = 0; a < L.naxes; ++a)
-      if (f.watch[a] && gate_open(f.watch[a])) atomicOr(f.viol, 1u);
-
-  const double tau = f.sc->tau, v = f.sc->v;
+  double ldx = 0.0;  // log det of factor (t >> 6) < 2: wave a sums its pivot-block terms
+  if (t < 128 && (t >> 6) < L.naxes)
+    for (int k = t & 63; k < f.nldet[t >> 6]; k += 64) ldx += f.ldet[t >> 6][k];
+  const double bgap = *f.bgap;  // boundary gap of U at the start of the step (assembly launch)
+  const double tau = f.sc->tau, v = f.sc->v, bc1 = f.sc->bc1, bc2 = f.sc->bc2;
   const double log_tau = f.params[L.off_tau], log_v = f.params[L.off_v];
+  int slot = 0;
+  bool gate = false;
+  if (t == 0) {
+    slot = *f.loss_slot;
+    if (f.viol)
+      for (int a = 0; a < L.naxes; ++a) gate |= f.watch[a] && gate_open(f.watch[a]);
+  }
+  // this thread's small parameters (kernel params of both axes, log_tau, log_v): value, Adam
+  // moments, and for kernel params the contracted field sum and the weight w_q
+  constexpr int PER = 2;  // nsmall <= 6 QMAX + 2 <= 2 * 256
+  double pp[PER], pm[PER], pv2[PER], pgx[PER], pw[PER];
+  int pidx[PER], pkind[PER];  // kind: 0 = kernel param, 1 = log_tau, 2 = log_v, -1 = none
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const int k = t + 256 * r;
+    pidx[r] = L.off_small + k;
+    pkind[r] = -1;
+    pp[r] = pm[r] = pv2[r] = pgx[r] = 0.0;
+    pw[r] = 1.0;
+    if (k >= L.nsmall) continue;
+    const int idx = pidx[r];
+    pp[r] = f.params[idx];
+    pm[r] = f.m[idx];
+    pv2[r] = f.v[idx];
+    if (idx == L.off_tau) { pkind[r] = 1; continue; }
+    if (idx == L.off_v) { pkind[r] = 2; continue; }
+    const int a = (L.naxes == 2 && idx >= L.off_kp[1]) ? 1 : 0;
+    const int rr = idx - L.off_kp[a], ty = rr / L.q, c = rr % L.q;  // ty: freq, log-ls, log-w
+    pkind[r] = 0;
+    pw[r] = f.kc[a].w[c];
+    pgx[r] = (ty == 0 && !f.has_cos) ? 0.0 : f.pg[a * 3 * QMAX + ty * QMAX + c];
+  }
+  // ---- phase 1: reductions, loss (thread 0)
+  if (t < 128) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ldx += __shfl_xor(ldx, o, 64);
+    if ((t & 63) == 0) sld[t >> 6] = ldx;
+  }
+  quad = block_sum(quad, sh);
+  egap = block_sum(egap, sh);  // (its barriers also publish sld)
   const double wb = f.llk_weight, c = f.logdet;
   if (t == 0) {
-    double ld[2] = {0.0, 0.0};
-    for (int a = 0; a < L.naxes; ++a)
-      for (int k = 0; k < f.nldet[a]; ++k) ld[a] += f.ldet[a][k];
+    if (gate) atomicOr(f.viol, 1u);
+    const double ld[2] = {sld[0], L.naxes > 1 ? sld[1] : 0.0};
     const double Nb = (L.dim == 2) ? (double)(2 * L.n2 + 2 * L.n1) : (double)f.nb;
     const double Nc = (L.dim == 2) ? (double)L.n1 * (double)L.n2 : (double)L.n1;
     double log_prior;
@@ -60,33 +100,25 @@ __device__ inline void finalize_body(const FinalizeArgs& f) {
     const double log_b = 0.5 * Nb * log_tau - 0.5 * tau * bgap;
     const double eq_ll = 0.5 * Nc * log_v - 0.5 * v * egap;
     const double loss = -(log_prior + log_b * wb + eq_ll);
-    f.grad[L.off_tau] = wb * (-0.5 * Nb + 0.5 * tau * bgap);
-    f.grad[L.off_v] = -0.5 * Nc + 0.5 * v * egap;
-    const int slot = *f.loss_slot;
+    sg[0] = wb * (-0.5 * Nb + 0.5 * tau * bgap);  // dL/dlog_tau
+    sg[1] = -0.5 * Nc + 0.5 * v * egap;           // dL/dlog_v
     f.losses[slot] = loss;
     *f.loss_slot = slot + 1;
     double* diag = f.diag;
     diag[0] = loss; diag[1] = ld[0]; diag[2] = ld[1]; diag[3] = quad; diag[4] = egap; diag[5] = bgap;
   }
-  // kernel-parameter gradients: fields were contracted without the weight w_q
-  for (int a = 0; a < L.naxes; ++a) {
-    const double* pg = f.pg + a * 3 * QMAX;
-    for (int k = t; k < L.q; k += 256) {
-      const double w = f.kc[a].w[k];
-      const int off = L.off_kp[a];
-      f.grad[off + k] = f.has_cos ? pg[k] * w : 0.0;          // freq
-      f.grad[off + L.q + k] = pg[QMAX + k] * w;                // log-ls
-      f.grad[off + 2 * L.q + k] = pg[2 * QMAX + k] * w;        // log-w
-    }
-  }
   __syncthreads();
-  if (f.apply) {
-    const double bc1 = f.sc->bc1, bc2 = f.sc->bc2;
-    for (int k = t; k < L.nsmall; k += 256) {
-      const int idx = L.off_small + k;
-      double p = f.params[idx], m = f.m[idx], vv = f.v[idx];
-      adam1(f.grad[idx], p, m, vv, f.hyper, bc1, bc2);
-      f.params[idx] = p; f.m[idx] = m; f.v[idx] = vv;
+  // ---- phase 2: gradients (kernel params: the fields were contracted without the weight w_q)
+  // and Adam on the small parameters
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    if (pkind[r] < 0) continue;
+    const double g = pkind[r] == 0 ? pgx[r] * pw[r] : sg[pkind[r] - 1];
+    const int idx = pidx[r];
+    f.grad[idx] = g;
+    if (f.apply) {
+      adam1(g, pp[r], pm[r], pv2[r], f.hyper, bc1, bc2);
+      f.params[idx] = pp[r]; f.m[idx] = pm[r]; f.v[idx] = pv2[r];
     }
   }
 }

@@ -18,6 +18,8 @@ GPK_FLAG_FORCE_SMALL_SPD = 4
 GPK_FLAG_FORCE_HUGE_GEMM = 8
 GPK_FLAG_NO_FAST_GRAPH = 16
 GPK_FLAG_FAST_FIRST = 32
+GPK_FLAG_NO_DCLASS = 64
+GPK_FLAG_NO_CHAIN = 128
 KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}
 EQ_IDS = {"poisson": 0, "allencahn": 1, "advection": 2}
 
@@ -86,6 +88,11 @@ EXPORTS = {
     "gpk_group_loss_grad": ([ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, _dp, _dp], ctypes.c_int),
     "gpk_shard_info": ([ctypes.c_void_p, _ip, _ip, _ip, _ip], ctypes.c_int),
     "gpk_graph_mode": ([ctypes.c_void_p, _ip, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
+    "gpk_distance_classes": ([_dp, ctypes.c_int32, _ip, _ip], ctypes.c_int),
+    "gpk_class_count": ([ctypes.c_void_p, ctypes.c_int32, _ip], ctypes.c_int),
+    "gpk_trace_reset": ([], ctypes.c_int),
+    "gpk_trace_read": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                        ctypes.c_int32], ctypes.c_int),
 }
 
 _LIB = None

@@ -48,6 +48,15 @@ def params_template(dim, n1, n2, Q):
             "kernel_paras_2": {k: v.copy() for k, v in kp.items()}, "log_tau": 0.0, "log_v": 0.0}
 
 
+def distance_classes(x):
+    """(ncls, vmax) of one axis' distance classes (host only; include/gpk.h
+    gpk_distance_classes).  ncls = 0: more than 32 distances on one diagonal."""
+    x = _lib.f64(x)
+    c, v = ctypes.c_int32(), ctypes.c_int32()
+    check(_lib.load().gpk_distance_classes(_lib.dptr(x), len(x), ctypes.byref(c), ctypes.byref(v)))
+    return int(c.value), int(v.value)
+
+
 class DeviceSolver:
     def __init__(self, dim, eq, kind, x1, src, bvals, x2=None, bidx=None, Q=30, jitter=1e-6,
                  llk_weight=200.0, logdet=True, beta=1.0, lr=0.01, freq_scale=20.0, device=0,
@@ -125,6 +134,15 @@ class DeviceSolver:
         return bool(f.value), int(r.value)
 
     # -- lifecycle ---------------------------------------------------------------------
+    def class_counts(self):
+        """Distance classes the step evaluates per axis (0: per-pair kernels)."""
+        out = []
+        for a in range(1 if self.dim == 1 else 2):
+            c = ctypes.c_int32()
+            check(_lib.load().gpk_class_count(self._h, a, ctypes.byref(c)))
+            out.append(int(c.value))
+        return out
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.load().gpk_destroy(self._h)

@@ -90,6 +90,15 @@ typedef struct gpk_problem {
  * bitwise those of the full graph. */
 #define GPK_FLAG_NO_FAST_GRAPH 16  /* always run the full graph */
 #define GPK_FLAG_FAST_FIRST 32     /* start in fast-graph mode (tests: exercises the rollback) */
+/* The step evaluates the covariance fields once per distinct pair distance |x_i - x_j| of each
+ * axis (exact fp64 classes, built at gpk_create; ~5n classes on a linspace grid instead of n^2
+ * pairs) and contracts the hyper-parameter gradient per class.  K and D are bitwise the per-pair
+ * evaluation's; the gradient sums differ only in summation order.  Grids with more than 32
+ * distinct distances on one diagonal |i - j| = k fall back to the per-pair kernels. */
+#define GPK_FLAG_NO_DCLASS 64      /* always use the per-pair kernels */
+/* Small factors (sum of (p/32)^2 over the factors <= 256) are inverted by ONE persistent
+ * launch whose workgroups order the pivot sweeps through flags; bitwise the per-sweep launches. */
+#define GPK_FLAG_NO_CHAIN 128      /* one launch per pivot sweep instead */
 
 typedef struct gpk_handle gpk_handle;
 
@@ -124,6 +133,19 @@ int gpk_destroy(gpk_handle* h);
 /* Graph selection state (see GPK_FLAG_NO_FAST_GRAPH): *fast = 1 if the next gpk_step uses the
  * fast graph, *rollbacks = batches rerun with the full graph so far.  Either pointer may be NULL. */
 int gpk_graph_mode(const gpk_handle* h, int32_t* fast, int64_t* rollbacks);
+
+/* Distance classes (GPK_FLAG_NO_DCLASS) of one coordinate axis x[n], host only (no device):
+ * *ncls = classes (distinct |x_i - x_j| per diagonal |i - j|), *vmax = the most on one diagonal;
+ * *ncls = 0 when that exceeds 32 (the step then uses the per-pair kernels).
+ * gpk_class_count: the classes a handle's step uses on axis 0 / 1 (0 = per-pair kernels). */
+int gpk_distance_classes(const double* x, int32_t n, int32_t* ncls, int32_t* vmax);
+int gpk_class_count(const gpk_handle* h, int32_t axis, int32_t* ncls);
+
+/* Latency-tuning probes (libgpk_trace.so, `make trace`; the product library returns GPK_EINVAL):
+ * per timeline slot (csrc/gpk_trace.h) the first-arrival / last-departure device clock
+ * (100 MHz) since the last gpk_trace_reset.  n >= 64. */
+int gpk_trace_reset(void);
+int gpk_trace_read(uint64_t* lo, uint64_t* hi, int32_t n);
 
 /* Flat parameter layout = jax's pytree leaf order (dict keys sorted):
  *   2D: [U (n1*n2, row-major), k1.freq[Q], k1.log-ls[Q], k1.log-w[Q],

@@ -1,0 +1,102 @@
+"""GPU: the distance-class step (include/gpk.h GPK_FLAG_NO_DCLASS; fields evaluated once per
+distinct |x_i - x_j|, hyper-parameter gradient contracted per class) against the per-pair
+kernels and the oracle.  The two paths evaluate the same closed forms at the same fp64
+distances; they differ only in the order in which mixture components and gradient terms are
+summed, so they agree to the rounding budget of the solves (cond(K) * eps)."""
+import numpy as np
+import pytest
+
+from oracle import gp_oracle as O
+from tests.helpers import device_solver, problem_1d, problem_2d, rel
+from tests.test_gpu_parity import _cmp_lossgrad, cond_tol
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(prob, Q, fs, params):
+    from gpk._lib import GPK_FLAG_NO_DCLASS
+    cls = device_solver(prob, Q, fs)
+    pair = device_solver(prob, Q, fs, flags=GPK_FLAG_NO_DCLASS)
+    for s in (cls, pair):
+        s.set_params(params)
+    assert all(c > 0 for c in cls.class_counts())
+    assert all(c == 0 for c in pair.class_counts())
+    return cls, pair
+
+
+def _u_mask(prob, params):
+    flat = O.flatten_params(params)
+    names = O.unflatten_params(params, np.arange(len(flat), dtype=np.float64))
+    key = "U" if "U" in names else "u"
+    m = np.zeros(len(flat), bool)
+    m[np.asarray(O.flatten_params(names[key]), dtype=int)] = True
+    return m
+
+
+CASES = [("1d", "poisson", "Matern52_Cos_1d"), ("1d", "allencahn", "SE_1d"),
+         ("2d", "poisson", "Matern52_Cos_1d"), ("2d", "allencahn", "SE_Cos_1d"),
+         ("2d", "advection", "Matern52_Cos_1d"), ("2d", "poisson", "Matern52_1d")]
+
+
+def _problem(dim, eq, kind):
+    if dim == "1d":
+        prob, params, _ = problem_1d(eq=eq, kind=kind, n=72, Q=6, seed=3)
+        return prob, params, 6, 20.0
+    prob, params, _, fs = problem_2d(eq=eq, kind=kind, n1=72, n2=40, Q=6, seed=3)
+    return prob, params, 6, fs
+
+
+@pytest.mark.parametrize("dim,eq,kind", CASES)
+def test_class_path_matches_pairs(dim, eq, kind):
+    prob, params, Q, fs = _problem(dim, eq, kind)
+    cls, pair = _pair(prob, Q, fs, params)
+    lc, gc = cls.loss_grad()
+    lp, gp = pair.loss_grad()
+    tol = cond_tol(prob, params)
+    assert abs(lc - lp) / abs(lp) < tol
+    m = _u_mask(prob, params)
+    assert rel(gc[m], gp[m]) < tol, rel(gc[m], gp[m])
+    assert rel(gc[~m], gp[~m]) < tol, rel(gc[~m], gp[~m])
+    cls.close()
+    pair.close()
+    _cmp_lossgrad(prob, params, Q, fs)  # and the oracle (class path: the default)
+
+
+@pytest.mark.parametrize("dim", ["1d", "2d"])
+def test_class_path_trajectory(dim):
+    prob, params, Q, fs = _problem(dim, "poisson", "Matern52_Cos_1d")
+    cls, pair = _pair(prob, Q, fs, params)
+    a, b = cls.step(20), pair.step(20)
+    assert np.max(np.abs(a - b) / np.abs(b)) < 1e-9
+    assert rel(cls.get_flat(), pair.get_flat()) < 1e-8
+    cls.close()
+    pair.close()
+
+
+def test_class_path_deterministic():
+    prob, params, Q, fs = _problem("2d", "poisson", "Matern52_Cos_1d")
+    out = []
+    for _ in range(2):
+        s = device_solver(prob, Q, fs)
+        s.set_params(params)
+        out.append((s.step(5), s.get_flat()))
+        s.close()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+
+
+def test_random_grid_uses_pairs_and_matches_oracle():
+    prob, params, Q, fs = _problem("2d", "poisson", "Matern52_Cos_1d")
+    rng = np.random.default_rng(7)
+    prob = dict(prob)
+    prob["x1"] = np.sort(rng.uniform(0, 2 * np.pi, len(prob["x1"])))
+    s = device_solver(prob, Q, fs)
+    assert s.class_counts() == [0, 0]  # axis 1 is scattered: both axes stay per-pair
+    s.close()
+    _cmp_lossgrad(prob, params, Q, fs)
+
+
+def test_c4_size_class_counts():
+    prob, params, _, fs = problem_2d(n1=256, n2=256, Q=30, seed=0)
+    s = device_solver(prob, 30, fs)
+    assert s.class_counts() == [1297, 1297]
+    s.close()

@@ -97,7 +97,10 @@ def test_rccl_single_rank_sharded_handle():
         ls, gs = s.loss_grad()
         assert abs(lr_ - ls) / abs(ls) < 1e-12
         assert rel(gr, gs) < 1e-10
-        assert rel(r.step(5), s.step(5)) < 1e-11
+        # the sharded step reduces the gradient partials in another order (reduce_parts +
+        # all-reduce vs the fused two-level tail): rounding-level gradient differences, which
+        # Adam's m/sqrt(v) can lift to ~1e-11 in the losses over 5 steps
+        assert rel(r.step(5), s.step(5)) < 1e-10
         assert rel(r.get_flat(), s.get_flat()) < 1e-10
     finally:
         r.close()

@@ -1,0 +1,59 @@
+"""One step's device timeline from the probe build (csrc/gpk_trace.h; `make -C ... trace`).
+
+    GPK_LIB_PATH=.../libgpk_trace.so python tools/timeline.py [--config C4] [--steps 3]
+
+Prints, per probed slot, [first arrival, last departure] in microseconds relative to the first
+probe of the step (100 MHz device clock, 10 ns resolution), averaged over --steps single steps.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process-slover-for-high-freq-pde_amd")]
+import numpy as np
+
+# single-workgroup probes (gpk_trace.h): "first" = workgroup 0, "last" = the last in the grid
+NAMES = {0: "class_eval first wg", 1: "gather pivot wg | chain wg(0,0)", 2: "pivot0 wait done", 3: "pivot0 factor",
+         40: "class_sum first wg", 41: "pgrad first wg start", 42: "pg first wg contracted",
+         43: "pg group tails", 44: "pg top tail", 45: "pg U plane wg0", 46: "pg finalize",
+         47: "pg last grad wg", 48: "pg first wg staged", 49: "class_sum last wg",
+         50: "class_eval last wg", 51: "gather last wg", 52: "class_sum wg0 loaded"}
+for k in range(16):
+    NAMES[4 + k] = f"sweep {k} (pivot wg)"
+    NAMES[20 + k] = f"  pivot in sweep {k}"
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="C4")
+ap.add_argument("--steps", type=int, default=5)
+a = ap.parse_args()
+if "GPK_LIB_PATH" not in os.environ:
+    os.environ["GPK_LIB_PATH"] = os.path.join(ROOT, "gaussian-process-slover-for-high-freq-pde_amd",
+                                              "gpk", "_lib", "libgpk_trace.so")
+from gpk import _lib, problems  # noqa: E402
+
+lib = _lib.load()
+s = problems.make_solver(a.config, seed=0)
+s.step(20)
+U64 = ctypes.c_uint64 * 64
+acc_lo, acc_hi, cnt = np.zeros(64), np.zeros(64), np.zeros(64)
+for _ in range(a.steps):
+    _lib.check(lib.gpk_trace_reset())
+    s.step(1)
+    lo, hi = U64(), U64()
+    _lib.check(lib.gpk_trace_read(lo, hi, 64))
+    lo = np.array(lo[:], dtype=np.float64)
+    hi = np.array(hi[:], dtype=np.float64)
+    valid_lo = lo < 2 ** 63
+    t0 = lo[valid_lo].min()
+    for i in range(64):
+        if hi[i] > 0 or valid_lo[i]:
+            acc_lo[i] += (lo[i] - t0) / 100.0 if valid_lo[i] else np.nan
+            acc_hi[i] += (hi[i] - t0) / 100.0 if hi[i] > 0 else np.nan
+            cnt[i] += 1
+print(f"{a.config}: one step, device timeline (us, mean of {a.steps})")
+for i in sorted(range(64), key=lambda i: (acc_lo[i] / max(cnt[i], 1)) if cnt[i] and not np.isnan(acc_lo[i]) else 1e9):
+    if cnt[i]:
+        l, h = acc_lo[i] / cnt[i], acc_hi[i] / cnt[i]
+        print(f"  {NAMES.get(i, i):24s} {l:9.2f} .. {h:9.2f}   ({h - l:7.2f})")
