@@ -10,10 +10,13 @@
 // K-steps of 32 staged through LDS; v_mfma_f64_16x16x4_f64 with the measured gfx950 map
 // (A[i=l&15][k=l>>4], B[k=l>>4][j=l&15], C/D row=(l>>4)+4r, col=l&15).
 #include "gpk_internal.h"
+#include "gpk_trace.h"
 
 #include <algorithm>
 
 namespace gpk {
+
+GPK_TRACE_TU(gemm)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int GSA = 34;  // A-role LDS stride (doubles)
@@ -61,19 +64,25 @@ __device__ __forceinline__ double block_sum_256(double v, double* red) {
 }
 
 // Epilogue operands of one output element, fetched early (their latency hides under MFMA).
+// Loads only -- no arithmetic on the loaded values here: a product formed at fetch time made
+// the compiler wait for each element's loads in turn (four serial round trips in wave 0 ahead
+// of its MFMA operand loads, ~4 us per latency-bound GEMM launch).
 struct EpiIn {
-  double pre, pu, q12;
+  double pre, pu, q1, q2;
 };
 
 __device__ __forceinline__ EpiIn epi_fetch(const GemmDesc& d, int row, int col) {
-  EpiIn e{0.0, 0.0, 0.0};
+  EpiIn e{0.0, 0.0, 0.0, 0.0};
   const size_t fo = (size_t)row * d.ldf + col;
   if ((d.epi == EPI_STORE || d.epi == EPI_QUAD) && d.beta != 0.0)
     e.pre = d.C0[(size_t)row * d.ldc0 + col];
   else if (d.epi == EPI_RESID)
     e.pre = d.F[fo];
   if (d.epi == EPI_QUAD || (d.epi == EPI_RESID && d.ac)) e.pu = d.U[fo];
-  if (d.epi == EPI_RESID && d.red2) e.q12 = d.Q1[fo] * d.Q2[fo];
+  if (d.epi == EPI_RESID && d.red2) {
+    e.q1 = d.Q1[fo];
+    e.q2 = d.Q2[fo];
+  }
   return e;
 }
 
@@ -88,7 +97,7 @@ __device__ __forceinline__ double epi_apply(const GemmDesc& d, double c, const E
       c -= e.pre;
       if (d.ac) c += e.pu * (e.pu * e.pu - 1.0);
       part += c * c;
-      part2 += e.q12;
+      part2 += e.q1 * e.q2;
       break;
     case EPI_QUAD:
       if (d.beta != 0.0) c += d.beta * e.pre;
@@ -204,6 +213,9 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
   const int i0 = (blockIdx.x / tn) * 16, j0 = (blockIdx.x % tn) * 16;
   __shared__ double part[2][4][256];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int tslot = SLOT_GEMM + 4 * (d.tag & 15);
+  if (TR_FIRST) TR_LO(tslot);
+  if (TR_LAST) TR_LO(tslot + 3);
   // K ranges are multiples of 32; wave wv takes a contiguous quarter (rounded to 32)
   auto range = [&](int K, int& b0, int& b1) {
     const int nk = K >> 5;
@@ -225,12 +237,14 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
     range(d.K2, b0, b1);
     acc2 = mma_chunk(d.A2, d.lda2, d.ta2, d.B2, d.ldb2, d.tb2, i0, j0, b0, b1, lane, acc2);
   }
+  if (TR_FIRST) TR_HI(tslot + 2);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     part[0][wv][lane * 4 + r] = acc1[r];
     part[1][wv][lane * 4 + r] = acc2[r];
   }
   __syncthreads();
+  if (TR_LAST) TR_HI(tslot + 3);
   if (wv != 0) return;
   double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
@@ -255,6 +269,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
     for (int o = 32; o > 0; o >>= 1) red2 += __shfl_xor(red2, o, 64);
     if (lane == 0) d.red2[blockIdx.x] = red2;
   }
+  if (TR_FIRST) TR_HI(tslot);
 }
 
 hipError_t launch_gemm_batch(const GemmDesc* descs, int ndesc, int max_tiles,

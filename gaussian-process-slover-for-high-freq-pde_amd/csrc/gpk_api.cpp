@@ -453,6 +453,7 @@ static int build_descs(gpk_handle* h) {
   const int force_big = gemm_force(h->prob.flags);
   auto end = [&](int k) {
     h->st[k].n = (int)d.size() - h->st[k].off;
+    for (int i = h->st[k].off; i < (int)d.size(); ++i) d[i].tag = k;
     h->st[k].gated = h->st[k].n > 0;
     for (int i = h->st[k].off; i < (int)d.size(); ++i) h->st[k].gated &= d[i].gate != nullptr;
     h->st[k].variant = gemm_variant(d.data() + h->st[k].off, h->st[k].n, force_big);
@@ -1454,18 +1455,20 @@ int gpk_trace_reset(void) {
   trace_reset_assemble();
   trace_reset_spdinv();
   trace_reset_pgrad();
+  trace_reset_gemm();
   return GPK_OK;
 }
 
 int gpk_trace_read(uint64_t* lo, uint64_t* hi, int32_t n) {
-  if (!lo || !hi || n < TRACE_SLOTS) return fail(GPK_EINVAL, "need 64 slots");
-  uint64_t l[3][TRACE_SLOTS], h[3][TRACE_SLOTS];
+  if (!lo || !hi || n < TRACE_SLOTS) return fail(GPK_EINVAL, "need 128 slots");
+  uint64_t l[4][TRACE_SLOTS], h[4][TRACE_SLOTS];
   trace_fetch_assemble(l[0], h[0]);
   trace_fetch_spdinv(l[1], h[1]);
   trace_fetch_pgrad(l[2], h[2]);
+  trace_fetch_gemm(l[3], h[3]);
   for (int i = 0; i < TRACE_SLOTS; ++i) {
-    lo[i] = std::min(l[0][i], std::min(l[1][i], l[2][i]));
-    hi[i] = std::max(h[0][i], std::max(h[1][i], h[2][i]));
+    lo[i] = std::min(std::min(l[0][i], l[3][i]), std::min(l[1][i], l[2][i]));
+    hi[i] = std::max(std::max(h[0][i], h[3][i]), std::max(h[1][i], h[2][i]));
   }
 #ifdef GPK_TRACE
   return GPK_OK;

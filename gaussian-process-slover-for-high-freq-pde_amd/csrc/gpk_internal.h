@@ -223,6 +223,7 @@ struct GemmDesc {
   double* red;              // per-tile partial sums, [tiles] (nullable)
   double* red2; const double* Q1; const double* Q2;  // EPI_RESID: sum Q1*Q2 (quad term)
   const double* gate; int ngate;  // refinement gate (gate_open); nullptr = always store
+  int tag;                  // step stage (timeline probes only, gpk_trace.h)
 };
 constexpr int GEMM_MAX_BATCH = 4;
 struct GemmBatch {  // passed by value (kernarg): no dependent descriptor load before the operands

@@ -11,7 +11,7 @@
 
 namespace gpk {
 
-constexpr int TRACE_SLOTS = 64;
+constexpr int TRACE_SLOTS = 128;
 enum TraceSlot {
   SLOT_CLASS_EVAL = 0, SLOT_GATHER = 1, SLOT_PIVOT0_WAIT = 2, SLOT_PIVOT0 = 3,
   SLOT_SWEEP = 4,         // + k (k < 16): whole sweep launch k
@@ -21,6 +21,8 @@ enum TraceSlot {
   // dispatch spread (last workgroup start) and intermediate points
   SLOT_PG_START = 47, SLOT_PG_STAGED = 48, SLOT_CSUM_START = 49, SLOT_CEVAL_START = 50,
   SLOT_GATHER_START = 51, SLOT_CSUM_LOADED = 52,
+  SLOT_GEMM = 64,  // + 4 * stage: first wg [start, end], + 1: first wg operands loaded,
+                   // + 2: first wg MFMAs done, + 3: last wg [start, end]  (stages < 16)
 };
 
 #ifdef GPK_TRACE
@@ -64,5 +66,7 @@ void trace_fetch_spdinv(uint64_t* lo, uint64_t* hi);
 void trace_reset_spdinv();
 void trace_fetch_pgrad(uint64_t* lo, uint64_t* hi);
 void trace_reset_pgrad();
+void trace_fetch_gemm(uint64_t* lo, uint64_t* hi);
+void trace_reset_gemm();
 
 }  // namespace gpk

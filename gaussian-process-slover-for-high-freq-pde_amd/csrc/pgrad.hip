@@ -147,45 +147,71 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
     vs = sc->v;
     hc = A.halfc;
   }
-  // operands of the ordered pair (i, j); ok = false: v = -1 (matches no variant).  Branch-free:
-  // out-of-range pairs load the clamped element (0, 0), so all loads of a 4-row group issue
-  // back to back instead of behind per-branch waits.
-  auto load = [&](bool ok, int i, int j, int& v, double& gk, double& gd) {
-    i = ok ? i : 0;
-    j = ok ? j : 0;
-    const size_t o = (size_t)i * p + j;
-    v = ok ? C.cid[o] - cb : -1;
-    if (MODE1D) {  // G_K = c/2 K^{-1} - 1/2 alpha alpha^T - v beta alpha^T, G_D = v R alpha^T
-      const double ai = A.alpha[i], aj = A.alpha[j];
-      gk = hc * A.Kinv[o] - 0.5 * ai * aj - vs * A.beta[i] * aj;
-      gd = vs * A.R[i] * aj;
-    } else {
-      gk = A.GK[o];
-      gd = A.GD[o];
-    }
-    if (DERIV == 1 && !(A.x[i] - A.x[j] >= 0.0)) gd = -gd;
-  };
+  // 8 ordered pairs per wave per pass (4 rows x lower / upper).  Addresses first, then every
+  // load of the pass back to back (cid, then the G operands), then the sums: one memory round
+  // trip per pass.  Out-of-range pairs load the clamped element (0, 0) and get v = -1, which
+  // matches no variant (bit-masked: a select on the loaded value let LLVM sink the load into an
+  // exec-masked branch behind a vmcnt(0) wait).
   for (int base = r0; base < r1; base += 16) {
-    int vl[4], vu[4];
-    double kl[4], dl[4], ku[4], du[4];
+    int ii[8], jj[8], msk[8];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int r = base + w + 4 * s;
       const bool in = kv && r < r1;
-      load(in && r >= k, r, r - k, vl[s], kl[s], dl[s]);
-      load(in && k > 0 && r + k < n, r, r + k, vu[s], ku[s], du[s]);
+      const bool lo = in && r >= k, up = in && k > 0 && r + k < n;
+      ii[2 * s] = lo ? r : 0;
+      jj[2 * s] = lo ? r - k : 0;
+      msk[2 * s] = -(int)lo;
+      ii[2 * s + 1] = up ? r : 0;
+      jj[2 * s + 1] = up ? r + k : 0;
+      msk[2 * s + 1] = -(int)up;
+    }
+    int cv[8];
+    double g0[8], g1[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) cv[s] = C.cid[(size_t)ii[s] * p + jj[s]];
+    if (MODE1D) {  // G_K = c/2 K^{-1} - 1/2 alpha alpha^T - v beta alpha^T, G_D = v R alpha^T
+      double ai[8], aj[8], bi[8], ri[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        g0[s] = A.Kinv[(size_t)ii[s] * p + jj[s]];
+        ai[s] = A.alpha[ii[s]];
+        aj[s] = A.alpha[jj[s]];
+        bi[s] = A.beta[ii[s]];
+        ri[s] = A.R[ii[s]];
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        g1[s] = vs * ri[s] * aj[s];
+        g0[s] = hc * g0[s] - 0.5 * ai[s] * aj[s] - vs * bi[s] * aj[s];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) g0[s] = A.GK[(size_t)ii[s] * p + jj[s]];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) g1[s] = A.GD[(size_t)ii[s] * p + jj[s]];
+    }
+    if (DERIV == 1) {
+      double xi[8], xj[8];
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        xi[s] = A.x[ii[s]];
+        xj[s] = A.x[jj[s]];
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (!(xi[s] - xj[s] >= 0.0)) g1[s] = -g1[s];
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < 8; ++s) {
+      const int v = ((cv[s] - cb) & msk[s]) | ~msk[s];
 #pragma unroll
       for (int x = 0; x < V; ++x) {
-        ak[x] += (vl[s] == x) ? kl[s] : 0.0;
-        ad[x] += (vl[s] == x) ? dl[s] : 0.0;
-        ak[x] += (vu[s] == x) ? ku[s] : 0.0;
-        ad[x] += (vu[s] == x) ? du[s] : 0.0;
+        ak[x] += (v == x) ? g0[s] : 0.0;
+        ad[x] += (v == x) ? g1[s] : 0.0;
       }
+    }
   }
-  if (TR_FIRST) TR_HI(SLOT_CSUM_LOADED);
   __shared__ double red[2][V][64];
 #pragma unroll
   for (int ww = 0; ww < 4; ++ww) {

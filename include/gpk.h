@@ -143,7 +143,7 @@ int gpk_class_count(const gpk_handle* h, int32_t axis, int32_t* ncls);
 
 /* Latency-tuning probes (libgpk_trace.so, `make trace`; the product library returns GPK_EINVAL):
  * per timeline slot (csrc/gpk_trace.h) the first-arrival / last-departure device clock
- * (100 MHz) since the last gpk_trace_reset.  n >= 64. */
+ * (100 MHz) since the last gpk_trace_reset.  n >= 128. */
 int gpk_trace_reset(void);
 int gpk_trace_read(uint64_t* lo, uint64_t* hi, int32_t n);
 

@@ -21,6 +21,11 @@ NAMES = {0: "class_eval first wg", 1: "gather pivot wg | chain wg(0,0)", 2: "piv
          47: "pg last grad wg", 48: "pg first wg staged", 49: "class_sum last wg",
          50: "class_eval last wg", 51: "gather last wg", 52: "class_sum wg0 loaded"}
 for k in range(16):
+    NAMES[64 + 4 * k] = f"gemm stage {k} first wg"
+    NAMES[65 + 4 * k] = f"  gemm {k} first wg loaded"
+    NAMES[66 + 4 * k] = f"  gemm {k} first wg mfma done"
+    NAMES[67 + 4 * k] = f"  gemm {k} last wg"
+for k in range(16):
     NAMES[4 + k] = f"sweep {k} (pivot wg)"
     NAMES[20 + k] = f"  pivot in sweep {k}"
 
@@ -36,24 +41,24 @@ from gpk import _lib, problems  # noqa: E402
 lib = _lib.load()
 s = problems.make_solver(a.config, seed=0)
 s.step(20)
-U64 = ctypes.c_uint64 * 64
-acc_lo, acc_hi, cnt = np.zeros(64), np.zeros(64), np.zeros(64)
+U64 = ctypes.c_uint64 * 128
+acc_lo, acc_hi, cnt = np.zeros(128), np.zeros(128), np.zeros(128)
 for _ in range(a.steps):
     _lib.check(lib.gpk_trace_reset())
     s.step(1)
     lo, hi = U64(), U64()
-    _lib.check(lib.gpk_trace_read(lo, hi, 64))
+    _lib.check(lib.gpk_trace_read(lo, hi, 128))
     lo = np.array(lo[:], dtype=np.float64)
     hi = np.array(hi[:], dtype=np.float64)
     valid_lo = lo < 2 ** 63
     t0 = lo[valid_lo].min()
-    for i in range(64):
+    for i in range(128):
         if hi[i] > 0 or valid_lo[i]:
             acc_lo[i] += (lo[i] - t0) / 100.0 if valid_lo[i] else np.nan
             acc_hi[i] += (hi[i] - t0) / 100.0 if hi[i] > 0 else np.nan
             cnt[i] += 1
 print(f"{a.config}: one step, device timeline (us, mean of {a.steps})")
-for i in sorted(range(64), key=lambda i: (acc_lo[i] / max(cnt[i], 1)) if cnt[i] and not np.isnan(acc_lo[i]) else 1e9):
+for i in sorted(range(128), key=lambda i: (acc_lo[i] / max(cnt[i], 1)) if cnt[i] and not np.isnan(acc_lo[i]) else 1e9):
     if cnt[i]:
         l, h = acc_lo[i] / cnt[i], acc_hi[i] / cnt[i]
         print(f"  {NAMES.get(i, i):24s} {l:9.2f} .. {h:9.2f}   ({h - l:7.2f})")
