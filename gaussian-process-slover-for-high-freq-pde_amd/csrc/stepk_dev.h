@@ -36,13 +36,21 @@ __device__ inline void finalize_body(const FinalizeArgs& f) {
   __shared__ double sh[4], sld[2], sg[2];
   const int t = threadIdx.x;
   const Layout& L = f.L;
-  // ---- phase 0: loads
-  double quad = 0.0, egap = 0.0;
-  for (int i = t; i < f.nquad; i += 256) quad += f.red_quad[i];
-  for (int i = t; i < f.negap; i += 256) egap += f.red_egap[i];
-  double ldx = 0.0;  // log det of factor (t >> 6) < 2: wave a sums its pivot-block terms
-  if (t < 128 && (t >> 6) < L.naxes)
-    for (int k = t & 63; k < f.nldet[t >> 6]; k += 64) ldx += f.ldet[t >> 6][k];
+  // ---- phase 0: loads.  The first pass of each partial sum is one unconditional load per
+  // thread (clamped index, masked value), so the quad / egap / log-det loads issue together;
+  // per-axis kernel-argument fields are chosen by uniform selects, not a dynamic index (which
+  // reads the kernarg block through memory, one more round trip).
+  const double* lp = ((t >> 6) == 1 && L.naxes > 1) ? f.ldet[1] : f.ldet[0];  // never null
+  const int nl = (t >> 6) >= L.naxes ? 0 : (t >> 6) == 1 ? f.nldet[1] : f.nldet[0];
+  const int lk = t & 63;
+  const double q0 = f.red_quad[t < f.nquad ? t : 0], e0 = f.red_egap[t < f.negap ? t : 0];
+  const double l0 = lp[lk < nl ? lk : 0];
+  double quad = t < f.nquad ? q0 : 0.0, egap = t < f.negap ? e0 : 0.0;
+  for (int i = t + 256; i < f.nquad; i += 256) quad += f.red_quad[i];
+  for (int i = t + 256; i < f.negap; i += 256) egap += f.red_egap[i];
+  double ldx = (t < 128 && lk < nl) ? l0 : 0.0;  // log det of factor t >> 6: its pivot blocks
+  if (t < 128)
+    for (int k = lk + 64; k < nl; k += 64) ldx += lp[k];
   const double bgap = *f.bgap;  // boundary gap of U at the start of the step (assembly launch)
   const double tau = f.sc->tau, v = f.sc->v, bc1 = f.sc->bc1, bc2 = f.sc->bc2;
   const double log_tau = f.params[L.off_tau], log_v = f.params[L.off_v];
