@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
   const int i0 = (blockIdx.x / tn) * 16, j0 = (blockIdx.x % tn) * 16;
   __shared__ double part[2][4][256];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int tslot = SLOT_GEMM + 4 * (d.tag & 15);
+  [[maybe_unused]] const int tslot = SLOT_GEMM + 4 * (d.tag & 15);
   if (TR_FIRST) TR_LO(tslot);
   if (TR_LAST) TR_LO(tslot + 3);
   // K ranges are multiples of 32; wave wv takes a contiguous quarter (rounded to 32)

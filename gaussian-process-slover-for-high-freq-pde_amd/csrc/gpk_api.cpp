@@ -121,7 +121,9 @@ struct gpk_handle {
                                       // update -> pivot hand-off counters (large path)
   bool bigspd = false;                // large-factor SPD inverse (spdinv_big.hip)
   bool chain = false;                 // small factors: persistent one-launch inverse (chain_kernel)
-  unsigned int* cflags[2] = {};       // its hand-off flags [T*T + T + 1] per factor
+  bool chain_aug = false;             // ... which also solves A, Bt^T and K^{-1} D^T (2D, unsharded)
+  unsigned int* cflags[2] = {};       // its hand-off flags [T*(T+taug) + T + 1] per factor
+  double *PD[2] = {}, *PBa[2] = {};   // K_a^{-1} D_a^T; augmented panel buffers
   ClassArgs cls[2] = {};              // distance classes per axis (ncls = 0: per-pair path)
   double* rvec = nullptr;            // 1D refinement residual
   double* uoff = nullptr;            // 1D Allen-Cahn offset (gpk_problem.uoff), or null
@@ -234,7 +236,16 @@ static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin) {
     c.n = a == 0 ? L.n1 : L.n2;
     if (gather) {
       c.cid = h->cls[a].cid; c.kval = h->cls[a].kval; c.dval = h->cls[a].dval;
-      c.x = a == 0 ? h->x1 : h->x2; c.jitter = h->prob.jitter; c.Kc = h->Kc[a]; c.D = h->D[a];
+      c.x = a == 0 ? h->x1 : h->x2; c.jitter = h->prob.jitter; c.Kc = h->Kc[a];
+    }
+    c.D = h->D[a];  // gather: written; read mode: the augmented D^T columns read it
+    if (h->chain_aug) {  // axis 0: [U | D1^T] -> A, K1^{-1} D1^T;  axis 1: [U^T | D2^T] -> Bt^T, P2
+      const int Po = a == 0 ? L.p2 : L.p1;
+      c.tu = Po / 32; c.td = c.p / 32;
+      c.Bu = h->Up; c.ldbu = L.p2; c.bu_t = a;
+      c.Ou = a == 0 ? h->A : h->Bt; c.ldou = L.p2; c.ou_t = a;
+      c.Od = h->PD[a]; c.ldod = c.p;
+      c.PBa = h->PBa[a]; c.ldpba = L.p1 + L.p2;
     }
     fin[a] = h->K[a];
   }
@@ -333,7 +344,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
   const int ac = h->prob.eq == GPK_ALLENCAHN;
   if (L.dim == 2) {
     for (int k = 0; k < kGemmStages; ++k) {
-      if (!refine && h->st[k].gated) continue;
+      if (h->st[k].n == 0 || (!refine && h->st[k].gated)) continue;
       TRY(check_launch(launch_gemm_auto(h->hdescs.data() + h->st[k].off, h->st[k].n, h->sc, h->s,
                                         h->st[k].variant), "gemm"));
       mark(h, stage++);
@@ -467,9 +478,12 @@ static int build_descs(gpk_handle* h) {
     return g;
   };
   // Stage A: A = K1^{-1} U, Bt = U K2^{-1}                       (2d.py:104-105)
+  // (augmented chain: both come out of the inverse launch itself -- no stage)
   begin(0);
-  d.push_back(mk(h->Kinv[0], P1, 0, h->Up, P2, 0, h->A, P2, P1, P2, P1));
-  d.push_back(mk(h->Up, P2, 0, h->Kinv[1], P2, 0, h->Bt, P2, P1, P2, P2));
+  if (!h->chain_aug) {
+    d.push_back(mk(h->Kinv[0], P1, 0, h->Up, P2, 0, h->A, P2, P1, P2, P1));
+    d.push_back(mk(h->Up, P2, 0, h->Kinv[1], P2, 0, h->Bt, P2, P1, P2, P2));
+  }
   end(0);
   begin(1);  // residuals W1 = U - K1 A, W2 = U - Bt K2
   {
@@ -520,12 +534,21 @@ static int build_descs(gpk_handle* h) {
   }
   end(5);
   // Stage C: T1 = beta D1^T R, T2 = R D2, G_D1 = v beta R A^T, G_D2 = v R^T Bt  (Appendix A)
+  // (augmented chain: X1 = beta (K1^{-1} D1^T) R and X2 = R (K2^{-1} D2^T)^T directly, from the
+  // inverse launch's K^{-1} D^T -- stage D's solves fold into this stage)
   begin(6);
-  {
+  if (h->chain_aug) {
+    GemmDesc x1 = mk(h->PD[0], P1, 0, h->R, P2, 0, h->X1, P2, P1, P2, P1);
+    x1.alpha = beta;
+    d.push_back(x1);
+    d.push_back(mk(h->R, P2, 0, h->PD[1], P2, 1, h->X2, P2, P1, P2, P2));
+  } else {
     GemmDesc t1 = mk(h->D[0], P1, 1, h->R, P2, 0, h->T1, P2, P1, P2, P1);
     t1.alpha = beta;
     d.push_back(t1);
     d.push_back(mk(h->R, P2, 0, h->D[1], P2, 0, h->T2, P2, P1, P2, P2));
+  }
+  {
     GemmDesc g = mk(h->R, P2, 0, h->A, P2, 1, h->GD[0], P1, P1, P1, P2);
     g.alpha = beta; g.vscale = 1;
     d.push_back(g);
@@ -536,11 +559,21 @@ static int build_descs(gpk_handle* h) {
   end(6);
   // Stage D: X1 = K1^{-1} T1, X2 = T2 K2^{-1} (refined)
   begin(7);
-  d.push_back(mk(h->Kinv[0], P1, 0, h->T1, P2, 0, h->X1, P2, P1, P2, P1));
-  d.push_back(mk(h->T2, P2, 0, h->Kinv[1], P2, 0, h->X2, P2, P1, P2, P2));
+  if (!h->chain_aug) {
+    d.push_back(mk(h->Kinv[0], P1, 0, h->T1, P2, 0, h->X1, P2, P1, P2, P1));
+    d.push_back(mk(h->T2, P2, 0, h->Kinv[1], P2, 0, h->X2, P2, P1, P2, P2));
+  }
   end(7);
-  begin(8);
-  {
+  begin(8);  // refinement residuals W1 = beta D1^T R - K1 X1, W2 = R D2 - X2 K2
+  if (h->chain_aug) {  // (T1, T2 never formed: dual products)
+    GemmDesc g = mk(h->D[0], P1, 1, h->R, P2, 0, h->W1, P2, P1, P2, P1);
+    g.alpha = beta;
+    g.A2 = h->Kc[0]; g.lda2 = P1; g.B2 = h->X1; g.ldb2 = P2; g.K2 = P1; g.alpha2 = -1.0;
+    d.push_back(gate(g, 0));
+    GemmDesc g2 = mk(h->R, P2, 0, h->D[1], P2, 0, h->W2, P2, P1, P2, P2);
+    g2.A2 = h->X2; g2.lda2 = P2; g2.B2 = h->Kc[1]; g2.ldb2 = P2; g2.K2 = P2; g2.alpha2 = -1.0;
+    d.push_back(gate(g2, 1));
+  } else {
     GemmDesc g = mk(h->Kc[0], P1, 0, h->X1, P2, 0, h->W1, P2, P1, P2, P1);
     g.alpha = -1.0; g.beta = 1.0; g.C0 = h->T1; g.ldc0 = P2;
     d.push_back(gate(g, 0));
@@ -1039,7 +1072,10 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     h->bigspd = (p->flags & GPK_FLAG_FORCE_BIG_SPD) != 0 ||
                 (!(p->flags & GPK_FLAG_FORCE_SMALL_SPD) && pmax >= SPD_BIG_MIN);
     const int pp[2] = {L.p1, L.p2};
-    h->chain = !h->bigspd && !(p->flags & GPK_FLAG_NO_CHAIN) && spd_chain_ok(pp, L.naxes);
+    h->chain = !h->bigspd && !(p->flags & GPK_FLAG_NO_CHAIN) &&
+               spd_chain_blocks(pp, L.naxes, false) <= CHAIN_MAX_BLOCKS;
+    h->chain_aug = h->chain && L.dim == 2 && !shard && !(p->flags & GPK_FLAG_NO_CHAIN_AUG) &&
+                   spd_chain_blocks(pp, L.naxes, true) <= CHAIN_MAX_BLOCKS;
   }
   auto bail = [&](int rc) {
     gpk_destroy(h);
@@ -1079,7 +1115,11 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     A_(h->Kc[a], (size_t)P * P);
     A_(h->pst[a], 2);
     A_(h->aflag[a], 1);
-    A_(h->cflags[a], (size_t)(P / 32) * (P / 32) + P / 32 + 1);
+    A_(h->cflags[a], (size_t)(P / 32) * (P / 32 + (P1 + P2) / 32) + P / 32 + 1);
+    if (h->chain_aug) {
+      A_(h->PD[a], (size_t)P * P);
+      A_(h->PBa[a], (size_t)P * (P1 + P2));
+    }
     h->nldet[a] = P / 32;
   }
   if (L.dim == 2) {

@@ -172,15 +172,26 @@ hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
 // Persistent ("chain") form of the small-factor inverse (spdinv.hip): every sweep in one launch,
 // ordered by flags; K^{-1} ends in X.  Gather mode (cid != nullptr) builds K from the distance
 // classes first and writes Kc and D on the way (no assembly launch); otherwise X holds K.
-constexpr int CHAIN_MAX_BLOCKS = 256;
+// Augmented form: extra tile columns carry right-hand sides B = [B_u | D^T] through the same
+// sweeps (the sweep operator's upper-right block), which end as K^{-1} B_u and K^{-1} D^T --
+// the step's first solves (A = K1^{-1} U, Bt^T = K2^{-1} U^T) and the derivative solves
+// (K^{-1} D^T) without GEMM launches of their own.
+// Every workgroup waits on others, so the grid must be co-resident: at most two per CU
+// (235 VGPRs, 50 KB LDS each fit twice).
+constexpr int CHAIN_MAX_BLOCKS = 512;
 struct ChainArgs {
   double* X; double* PB; double* piv; double* ldet; double* pst; int* status;
-  unsigned int* flags;  // [T*T + T + 1], zero-initialised
+  unsigned int* flags;  // [T*(T+tu+td) + T + 1], zero-initialised
   int p, n;
   const int* cid; const double* kval; const double* dval; const double* x; double jitter;
   double* Kc; double* D;
+  int tu, td;                              // augmented tile columns: B_u, D^T (0: none)
+  const double* Bu; int ldbu, bu_t;        // B_u[i][j] = bu_t ? Bu[j*ldbu+i] : Bu[i*ldbu+j]
+  double* Ou; int ldou, ou_t;              // K^{-1} B_u (stored transposed when ou_t)
+  double* Od; int ldod;                    // K^{-1} D^T
+  double* PBa; int ldpba;                  // augmented panel buffer [p][32*(tu+td)]
 };
-bool spd_chain_ok(const int* p, int nmat);
+int spd_chain_blocks(const int* p, int nmat, bool aug);
 hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s);
 
 // Large-factor path (spdinv_big.hip): 64-wide pivots, panel + lower-tile MFMA update per sweep,

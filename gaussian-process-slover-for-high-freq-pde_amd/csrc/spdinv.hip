@@ -218,6 +218,13 @@ struct ChainFactor {
   // gather mode: K from the distance classes (+ jitter), kept copy Kc and D written on the way
   const int* cid; const double* kval; const double* dval; const double* x; double jitter;
   double* Kc; double* D;
+  // augmented right-hand sides: tile columns T.. of the sweep operator's upper-right block end
+  // as K^{-1} [B_u | D^T]  (gpk_internal.h ChainArgs)
+  int tu, td;
+  const double* Bu; int ldbu, bu_t;
+  double* Ou; int ldou, ou_t;
+  double* Od; int ldod;
+  double* PBa; int ldpba;
 };
 struct ChainBatch {
   ChainFactor f[2];
@@ -245,15 +252,23 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   const int m = blockIdx.y;
   const ChainFactor& F = b.f[m];
   const int T = F.T, p = F.p;
+  const int TC = T + F.tu + F.td;  // tile columns: K, then the augmented B_u, D^T columns
   const int tile = blockIdx.x;
-  if (tile >= T * T) return;
-  const int I = tile / T, J = tile % T;
+  if (tile >= T * TC) return;
+  const int I = tile / TC, J = tile % TC;
+  const bool aug = J >= T;
+  const int ja = J - T;  // augmented tile column
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int tx = t & 31, ty = t >> 5;
   unsigned int* panel_rdy = F.flags;
-  unsigned int* piv_rdy = F.flags + T * T;
-  unsigned int* done = F.flags + T * T + T;
+  unsigned int* piv_rdy = F.flags + T * TC;
+  unsigned int* done = F.flags + T * TC + T;
+  // panel tile (row k) of column J: K part in PB, augmented part in PBa
+  auto panel_ptr = [&](int k, int row, int col) -> double* {
+    return J < T ? F.PB + (size_t)(k * 32 + row) * p + J * 32 + col
+                 : F.PBa + (size_t)(k * 32 + row) * F.ldpba + ja * 32 + col;
+  };
   __shared__ double sL[32 * SA];
   __shared__ double sXI[32 * SB], sXJ[32 * SB];
   __shared__ double sP[32 * SP], sM[32 * SP], pv[32];
@@ -265,6 +280,24 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   for (int r = 0; r < 4; ++r) {
     const int i = I * 32 + 16 * wr + (lane >> 4) + 4 * r, j = J * 32 + 16 * wc + (lane & 15);
     const size_t o = (size_t)i * p + j;
+    if (aug) {  // B_u[i][j'] or D^T[i][j'] = D[j'][i] (j' = column inside the part)
+      const int jl = ja * 32 + 16 * wc + (lane & 15);
+      if (ja < F.tu) {
+        acc[r] = F.bu_t ? F.Bu[(size_t)(jl) * F.ldbu + i] : F.Bu[(size_t)i * F.ldbu + jl];
+      } else {
+        const int jd = jl - 32 * F.tu;
+        const size_t od = (size_t)jd * p + i;
+        if (GATHER) {
+          const int u = F.cid[od];
+          double dv = u >= 0 ? F.dval[u] : 0.0;
+          if (DERIV == 1 && u >= 0 && !(F.x[jd] - F.x[i] >= 0.0)) dv = -dv;
+          acc[r] = dv;
+        } else {
+          acc[r] = F.D[od];
+        }
+      }
+      continue;
+    }
     if (GATHER) {
       const int u = F.cid[o];
       double kv, dv;
@@ -284,12 +317,10 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
       acc[r] = F.X[o];
     }
   }
-  auto publish_tile = [&](void) {  // PB tile (I, J) <- acc, then its flag
+  auto publish_tile = [&](void) {  // panel tile (I, J) <- acc, then its flag
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      st_sc1(F.PB + (size_t)(I * 32 + 16 * wr + (lane >> 4) + 4 * r) * p + J * 32 + 16 * wc + (lane & 15),
-             acc[r]);
-    signal_flag(panel_rdy + I * T + J);
+    for (int r = 0; r < 4; ++r) st_sc1(panel_ptr(I, 16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15)), acc[r]);
+    signal_flag(panel_rdy + I * TC + J);
   };
   const bool trm = t == 0 && m == 0;  // probes (gpk_trace.h): factor 0's pivot owners
   auto factor_pivot = [&](int kp, bool with_tile) {  // acc: Schur complement of pivot block kp
@@ -297,9 +328,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     __syncthreads();
     if (with_tile) {  // this tile as the panel of sweep kp (its stores drain with the pivot's)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        st_sc1(F.PB + (size_t)(I * 32 + 16 * wr + (lane >> 4) + 4 * r) * p + J * 32 + 16 * wc + (lane & 15),
-               acc[r]);
+      for (int r = 0; r < 4; ++r) st_sc1(panel_ptr(I, 16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15)), acc[r]);
     }
     if (trm && kp > 0 && kp < 17) TR_LO(SLOT_SWEEP_PIVOT + kp - 1);
     if (trm && kp == 0) TR_LO(SLOT_PIVOT0);
@@ -309,7 +338,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
-      if (with_tile) __hip_atomic_store(panel_rdy + I * T + J, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (with_tile) __hip_atomic_store(panel_rdy + I * TC + J, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(piv_rdy + kp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP_PIVOT + kp - 1);
@@ -332,8 +361,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     // the panel tiles are usually published long before the pivot: fetch them first, then
     // wait for L^{-1}_k
     if (t == 0) {
-      if (needI) wait_flag(panel_rdy + k * T + I);
-      if (needJ) wait_flag(panel_rdy + k * T + J);
+      if (needI) wait_flag(panel_rdy + k * TC + I);
+      if (needJ) wait_flag(panel_rdy + k * TC + J);
     }
     __syncthreads();
     double xi[4], xj[4];
@@ -341,7 +370,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     for (int r = 0; r < 4; ++r) {
       const int row = ty + 8 * r;
       xi[r] = needI ? ld_sc1(F.PB + (size_t)(k * 32 + row) * p + I * 32 + tx) : 0.0;
-      xj[r] = needJ ? ld_sc1(F.PB + (size_t)(k * 32 + row) * p + J * 32 + tx) : 0.0;
+      xj[r] = needJ ? ld_sc1(panel_ptr(k, row, tx)) : 0.0;
     }
     if (t == 0) {
       wait_flag(piv_rdy + k);
@@ -386,9 +415,21 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     }
     __syncthreads();  // LDS is refilled next sweep
   }
+  if (aug) {  // upper-right block: +K^{-1} B (B_u part possibly stored transposed)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = I * 32 + 16 * wr + (lane >> 4) + 4 * r, jl = ja * 32 + 16 * wc + (lane & 15);
+      if (ja < F.tu) {
+        if (F.ou_t) F.Ou[(size_t)jl * F.ldou + i] = acc[r];
+        else F.Ou[(size_t)i * F.ldou + jl] = acc[r];
+      } else {
+        F.Od[(size_t)i * F.ldod + jl - 32 * F.tu] = acc[r];
+      }
+    }
+  }
   // K^{-1} = -X after the last sweep
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < 4 && !aug; ++r) {
     const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
     const double y = -acc[r];
     F.X[(size_t)(I * 32 + row) * p + J * 32 + col] = y;
@@ -402,19 +443,20 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   }
   if (trm && tile == 0) TR_HI(SLOT_GATHER);
   // the last workgroup of this factor re-arms the flags for the next launch
-  if (t == 0) s_last = atomicAdd(done, 1u) == (unsigned)(T * T - 1);
+  if (t == 0) s_last = atomicAdd(done, 1u) == (unsigned)(T * TC - 1);
   __syncthreads();
   if (s_last) {
-    for (int e = t; e < T * T + T; e += 256)
+    for (int e = t; e < T * TC + T; e += 256)
       __hip_atomic_store(F.flags + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-bool spd_chain_ok(const int* p, int nmat) {
-  int blocks = 0;
-  for (int m = 0; m < nmat; ++m) blocks += (p[m] / 32) * (p[m] / 32);
-  return blocks <= CHAIN_MAX_BLOCKS;
+int spd_chain_blocks(const int* p, int nmat, bool aug) {
+  int blocks = 0, cols = 0;
+  for (int m = 0; m < nmat; ++m) cols += p[m] / 32;
+  for (int m = 0; m < nmat; ++m) blocks += (p[m] / 32) * (p[m] / 32 + (aug ? cols : 0));
+  return blocks;
 }
 
 hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s) {
@@ -427,10 +469,13 @@ hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t
     f.status = a[m].status; f.flags = a[m].flags; f.p = a[m].p; f.n = a[m].n; f.T = a[m].p / 32;
     f.cid = a[m].cid; f.kval = a[m].kval; f.dval = a[m].dval; f.x = a[m].x; f.jitter = a[m].jitter;
     f.Kc = a[m].Kc; f.D = a[m].D;
+    f.tu = a[m].tu; f.td = a[m].td; f.Bu = a[m].Bu; f.ldbu = a[m].ldbu; f.bu_t = a[m].bu_t;
+    f.Ou = a[m].Ou; f.ldou = a[m].ldou; f.ou_t = a[m].ou_t; f.Od = a[m].Od; f.ldod = a[m].ldod;
+    f.PBa = a[m].PBa; f.ldpba = a[m].ldpba;
     if ((a[m].cid != nullptr) != gather) return hipErrorInvalidValue;
-    Tmax = std::max(Tmax, f.T);
+    Tmax = std::max(Tmax, f.T * (f.T + f.tu + f.td));
   }
-  dim3 grid(Tmax * Tmax, nmat);
+  dim3 grid(Tmax, nmat);
   if (!gather)
     hipLaunchKernelGGL((chain_kernel<0, false>), grid, dim3(256), 0, s, b);
   else if (deriv == 1)

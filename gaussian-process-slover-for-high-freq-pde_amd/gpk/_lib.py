@@ -20,6 +20,7 @@ GPK_FLAG_NO_FAST_GRAPH = 16
 GPK_FLAG_FAST_FIRST = 32
 GPK_FLAG_NO_DCLASS = 64
 GPK_FLAG_NO_CHAIN = 128
+GPK_FLAG_NO_CHAIN_AUG = 256
 KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}
 EQ_IDS = {"poisson": 0, "allencahn": 1, "advection": 2}
 

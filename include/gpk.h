@@ -99,6 +99,10 @@ typedef struct gpk_problem {
 /* Small factors (sum of (p/32)^2 over the factors <= 256) are inverted by ONE persistent
  * launch whose workgroups order the pivot sweeps through flags; bitwise the per-sweep launches. */
 #define GPK_FLAG_NO_CHAIN 128      /* one launch per pivot sweep instead */
+/* 2D, unsharded, chain-sized: the inverse launch also carries U, U^T and D^T as augmented
+ * columns of the sweep operator and ends with A = K1^{-1} U, Bt = U K2^{-1} and K^{-1} D^T,
+ * which replace the step's first GEMM stage and fold the X1/X2 solves into the G_D stage. */
+#define GPK_FLAG_NO_CHAIN_AUG 256  /* the chain inverts K only */
 
 typedef struct gpk_handle gpk_handle;
 

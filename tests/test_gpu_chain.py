@@ -2,7 +2,9 @@
 include/gpk.h GPK_FLAG_NO_CHAIN) against the one-launch-per-sweep inverse.  It performs the
 same operations in the same order, so loss, gradient and Adam trajectories are bitwise equal --
 with the distance-class gather (K, Kc, D built inside the inverse launch) and with the per-pair
-assembly alike."""
+assembly alike.  The augmented form (GPK_FLAG_NO_CHAIN_AUG; A = K1^{-1} U, Bt, K^{-1} D^T out
+of the same sweeps) solves by the sweep operator instead of explicit-inverse GEMMs: it agrees
+with the oracle and the GEMM form to the solves' rounding budget."""
 import numpy as np
 import pytest
 
@@ -31,9 +33,9 @@ def _case(name):
 @pytest.mark.parametrize("name", ["1d", "1d_ac", "2d", "adv", "c4"])
 @pytest.mark.parametrize("dclass", [True, False])
 def test_chain_bitwise_sweeps(name, dclass):
-    from gpk._lib import GPK_FLAG_NO_CHAIN, GPK_FLAG_NO_DCLASS
+    from gpk._lib import GPK_FLAG_NO_CHAIN, GPK_FLAG_NO_CHAIN_AUG, GPK_FLAG_NO_DCLASS
     prob, params, Q, fs = _case(name)
-    base = 0 if dclass else GPK_FLAG_NO_DCLASS
+    base = (0 if dclass else GPK_FLAG_NO_DCLASS) | GPK_FLAG_NO_CHAIN_AUG
     a = device_solver(prob, Q, fs, flags=base)
     b = device_solver(prob, Q, fs, flags=base | GPK_FLAG_NO_CHAIN)
     for s in (a, b):
@@ -60,3 +62,28 @@ def test_chain_repeated_launches_rearm():
     assert np.array_equal(la, lb)
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("name", ["2d", "adv", "c4"])
+@pytest.mark.parametrize("dclass", [True, False])
+def test_chain_aug_matches_gemm_form_and_oracle(name, dclass):
+    from gpk._lib import GPK_FLAG_NO_CHAIN_AUG, GPK_FLAG_NO_DCLASS
+    from tests.helpers import rel
+    from tests.test_gpu_parity import _cmp_lossgrad, cond_tol
+    prob, params, Q, fs = _case(name)
+    base = 0 if dclass else GPK_FLAG_NO_DCLASS
+    a = device_solver(prob, Q, fs, flags=base)
+    b = device_solver(prob, Q, fs, flags=base | GPK_FLAG_NO_CHAIN_AUG)
+    for s in (a, b):
+        s.set_params(params)
+    la, ga = a.loss_grad()
+    lb, gb = b.loss_grad()
+    tol = cond_tol(prob, params)
+    assert abs(la - lb) / abs(lb) < tol
+    assert rel(ga, gb) < tol, rel(ga, gb)
+    sa, sb = a.step(10), b.step(10)
+    assert np.max(np.abs(sa - sb) / np.abs(sb)) < 1e-8
+    a.close()
+    b.close()
+    if name != "c4":
+        _cmp_lossgrad(prob, params, Q, fs, flags=base)
