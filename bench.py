@@ -31,14 +31,17 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process-slover-for-high-freq-
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_F64_TFLOPS = 78.6    # MI355X fp64 dense matrix (= vector) peak, spec
 METRIC = "log-joint iters/sec + fp64 Cholesky GFLOP/s, 2D Poisson 256^2, 1-8 GPU"
-KERNEL_LAUNCHES = {"sweep": None, "gemm_B": 5, "pgrad": 1, "assemble": 1}  # per step (sweep: T)
+# launches per step of the fast step graph (sweep: T = p/32 in the per-sweep inverse; the
+# persistent chain inverse is one launch; 3 GEMM stages with the augmented chain, else 5)
+KERNEL_LAUNCHES = {"spd_chain": 1, "sweep": None, "gemm_B": 3, "pgrad": 1, "assemble": 1}
 
 
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench (tools/gpu_round.sh), summarised by
 # tools/pmc_summary.py: HBM-side bytes per launch (2*FETCH + WRITE, MI355X_MICROARCH.md §HBM)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r1_pmc_c4.json")
-PMC_KERNEL = {"sweep": "gpk::sweep_kernel", "gemm_B": "gpk::gemm_small_kernel",
-              "pgrad": "gpk::pgrad_kernel<true, true, 2, false>", "assemble": "gpk::assemble_kernel<true, true, 2>"}
+PMC_KERNEL = {"spd_chain": "gpk::chain_kernel<2, true>", "sweep": "gpk::sweep_kernel",
+              "gemm_B": "gpk::gemm_small_kernel", "pgrad": "gpk::pgrad_kernel<true, true, 2, false, true>",
+              "assemble": "gpk::class_eval_kernel<true, true, 2>"}
 
 
 def pmc_traffic(kernel):
@@ -189,7 +192,12 @@ def main():
     # per-kernel timings; the dominant kernel = largest device time per step
     T = (n + 31) // 32
     kern = {}
-    for name in (["sweep", "gemm_B", "pgrad", "assemble"] if cfg["dim"] == 2 else ["sweep", "assemble"]):
+    try:  # the step's SPD inverse: the persistent chain launch when the factors are small
+        s.bench_kernel("spd_chain", 1)
+        spd = "spd_chain"
+    except Exception:
+        spd = "sweep"
+    for name in ([spd, "gemm_B", "pgrad", "assemble"] if cfg["dim"] == 2 else [spd, "assemble"]):
         us, fl, by = s.bench_kernel(name, a.kernel_iters)
         launches = T if name == "sweep" else KERNEL_LAUNCHES[name]
         kern[name] = dict(us=us, flops=fl, bytes=by, per_step_us=us * launches)

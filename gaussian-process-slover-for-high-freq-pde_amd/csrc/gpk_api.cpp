@@ -225,7 +225,7 @@ static void fill_spd(gpk_handle* h, SpdArgs* sa) {
 }
 
 // the persistent small-factor inverse; gather: K (+ Kc, D) straight from the distance classes
-static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin) {
+static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin, bool aug = true) {
   const Layout& L = h->L;
   ChainArgs ca[2] = {};
   for (int a = 0; a < L.naxes; ++a) {
@@ -239,7 +239,7 @@ static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin) {
       c.x = a == 0 ? h->x1 : h->x2; c.jitter = h->prob.jitter; c.Kc = h->Kc[a];
     }
     c.D = h->D[a];  // gather: written; read mode: the augmented D^T columns read it
-    if (h->chain_aug) {  // axis 0: [U | D1^T] -> A, K1^{-1} D1^T;  axis 1: [U^T | D2^T] -> Bt^T, P2
+    if (h->chain_aug && aug) {  // axis 0: [U | D1^T] -> A, K1^{-1} D1^T;  axis 1: [U^T | D2^T] -> Bt^T, P2
       const int Po = a == 0 ? L.p2 : L.p1;
       c.tu = Po / 32; c.td = c.p / 32;
       c.Bu = h->Up; c.ldbu = L.p2; c.bu_t = a;
@@ -256,7 +256,7 @@ static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin) {
 // assembly launch; large: 64-wide panel/update sweeps)
 static hipError_t launch_inverse(gpk_handle* h, SpdArgs* sa, double** fin, bool pivot0_done) {
   if (h->bigspd) return launch_spd_inverse_big(sa, h->L.naxes, fin, h->s);
-  if (h->chain) return launch_chain(h, false, fin);
+  if (h->chain) return launch_chain(h, false, fin, false);  // K^{-1} only (timing, predict)
   return launch_spd_inverse(sa, h->L.naxes, fin, h->s, pivot0_done);
 }
 
@@ -1861,7 +1861,26 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
   std::function<hipError_t()> launch;
   double flops = 0.0, bytes = 0.0;
   const double n1 = L.n1, n2 = L.dim == 2 ? L.n2 : 0.0;
-  if (nm == "sweep" && h->bigspd) {
+  if (nm == "spd_chain") {
+    // the step's persistent inverse launch as the step runs it (gather mode after the class
+    // values; idempotent: it rebuilds K from the classes each time)
+    if (!h->chain) return fail(GPK_EINVAL, "spd_chain: this handle does not use the chain inverse");
+    const bool gather = h->cls[0].ncls > 0;
+    for (int a = 0; a < L.naxes; ++a) aa[a].cls = h->cls[a];
+    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s, gather),
+                     "assemble"));
+    launch = [&, gather]() {
+      double* fin[2];
+      return launch_chain(h, gather, fin);
+    };
+    // potrf + potri = n^3 per factor; each augmented column a triangular solve pair, 2 n^2
+    // bytes: K^{-1}, Kc, D written (24 n^2), augmented outputs written (8 n m), U read
+    for (int a = 0; a < L.naxes; ++a) {
+      const double n = a == 0 ? n1 : n2, m = h->chain_aug ? n1 + n2 : 0.0;
+      flops += n * n * n + 2.0 * n * n * m;
+      bytes += 24.0 * n * n + 8.0 * n * m + (h->chain_aug ? 8.0 * n1 * n2 : 0.0);
+    }
+  } else if (nm == "sweep" && h->bigspd) {
     // large path: time the update launch of sweep 0 (in place, so every timed launch gets a
     // freshly assembled K, pivot 0 and panel 0 first; only the update is between the events)
     hipEvent_t e0, e1;
@@ -1923,7 +1942,12 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
       bytes += 16.0 * n * n;
     }
   } else if (nm == "assemble") {
-    launch = [&]() { return launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s); };
+    // the step's assembly launch(es): class values only when the chain gathers K itself
+    const bool eval_only = h->chain && h->cls[0].ncls > 0;
+    for (int a = 0; a < L.naxes; ++a) aa[a].cls = h->cls[a];
+    launch = [&, eval_only]() {
+      return launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s, eval_only);
+    };
     // K and D written (8 B each per element); flops not counted (transcendental-bound)
     for (int a = 0; a < L.naxes; ++a) { const double n = a == 0 ? n1 : n2; bytes += 16.0 * n * n; }
   } else if (nm == "gemm_B" && L.dim == 2) {
@@ -1946,7 +1970,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     launch = [&, pa]() mutable { return launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s); };
     bytes = 16.0 * (n1 * n1 + n2 * n2);  // G_K, G_D read
   } else {
-    return fail(GPK_EINVAL, "unknown kernel name (sweep | assemble | gemm_B | pgrad[2D])");
+    return fail(GPK_EINVAL, "unknown kernel name (spd_chain | sweep | assemble | gemm_B | pgrad[2D])");
   }
   HIPCHK(launch());  // warm
   hipEvent_t e0, e1;

@@ -15,6 +15,10 @@ import pytest
 from oracle import gp_oracle as O
 from tests.helpers import device_solver, problem_2d, rel
 
+# Sharded handles solve A = K1^{-1} U etc. by GEMMs against K^{-1}; an unsharded handle folds
+# those solves into its inverse launch (GPK_FLAG_NO_CHAIN_AUG) -- compare like with like.
+from gpk._lib import GPK_FLAG_NO_CHAIN_AUG as NO_AUG  # noqa: E402
+
 
 def _group(prob, Q, fs, nranks, flags=0):
     from gpk.core import DeviceGroup
@@ -40,7 +44,7 @@ def test_group_loss_grad(eq, kind, n1, n2, nranks):
     (unequal axes, ragged last row blocks, padding to 32 * nranks)."""
     prob, params, _, fs = problem_2d(eq=eq, kind=kind, n1=n1, n2=n2, Q=5, seed=21)
     g = _group(prob, 5, fs, nranks)
-    s = device_solver(prob, 5, fs)
+    s = device_solver(prob, 5, fs, flags=NO_AUG)  # the sharded step's own algorithm
     try:
         g.set_params(params)
         s.set_params(params)
@@ -64,7 +68,7 @@ def test_group_trajectory_matches_unsharded(nranks, flags):
     forces the 128x128 GEMM where the row blocks allow it (downgraded per stage otherwise)."""
     prob, params, (Xte, _), fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=200, n2=136, Q=6, seed=3)
     g = _group(prob, 6, fs, nranks, flags=flags)
-    s = device_solver(prob, 6, fs)
+    s = device_solver(prob, 6, fs, flags=NO_AUG)
     try:
         g.set_params(params)
         s.set_params(params)
@@ -88,7 +92,7 @@ def test_rccl_single_rank_sharded_handle():
               logdet=prob["logdet"], lr=0.01, freq_scale=fs)
     r = DeviceSolver(2, prob["eq"], prob["kind"], prob["x1"], prob["src"], prob["bvals"],
                      shard=(0, 1, comm_unique_id()), **kw)
-    s = device_solver(prob, 4, fs)
+    s = device_solver(prob, 4, fs, flags=NO_AUG)
     try:
         assert r.shard_info() == (0, 1, 0, 64)
         r.set_params(params)
