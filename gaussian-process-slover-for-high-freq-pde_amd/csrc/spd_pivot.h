@@ -9,7 +9,8 @@ constexpr int SP = 33;  // pivot scratch stride
 typedef __attribute__((address_space(3))) double* lds_ptr;
 
 __device__ __forceinline__ double rsqrt_f64(double p) {
-  double y = __builtin_amdgcn_rsq(p);          // ~2^-29 relative
+  double y = __builtin_amdgcn_rsq(p);          // 2^-24.2 relative (tools/probes/rsq_probe.hip):
+                                               // one Newton step leaves 4e-15, two 1.4e-16
   double e = fma(-p * y, y, 1.0);              // 1 - p y^2
   y = fma(0.5 * y, e, y);
   e = fma(-p * y, y, 1.0);
