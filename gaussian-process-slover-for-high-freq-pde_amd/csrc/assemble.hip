@@ -18,6 +18,7 @@
 #include "gpk_internal.h"
 #include "spd_pivot.h"
 #include "gpk_trace.h"
+#include "prep_dev.h"
 
 namespace gpk {
 
@@ -66,76 +67,6 @@ struct AssembleBatch {
   int pivot_x;    // blockIdx.x of the pivot-0 workgroup (per axis), or -1
   PrepArgs prep;
 };
-
-// exp of the params -> axis constants of component c (prep2 semantics, bitwise)
-__device__ __forceinline__ void axis_component(const PrepArgs& P, int axis, int q, int c, double& w,
-                                               double& a, double& om) {
-  const int off = P.off_kp[axis];
-  om = TWO_PI * P.params[off + c];          // freq
-  a = exp(P.params[off + q + c]);           // log-ls
-  w = exp(P.params[off + 2 * q + c]);       // log-w
-}
-
-// workgroup (0, 0): publish the step constants for the later kernels of the step
-__device__ void publish_prep(const PrepArgs& P, int q) {
-  const int t = threadIdx.x;
-  for (int ax = 0; ax < P.naxes; ++ax)
-    for (int c = t; c < q; c += blockDim.x) {
-      double w, a, om;
-      axis_component(P, ax, q, c, w, a, om);
-      P.kc[ax].om[c] = om;
-      P.kc[ax].a[c] = a;
-      P.kc[ax].w[c] = w;
-    }
-  if (t == 0) {
-    P.sc->tau = exp(P.params[P.off_tau]);
-    P.sc->v = exp(P.params[P.off_v]);
-    const int n = *P.count + 1;
-    if (P.apply) *P.count = n;
-    P.sc->bc1 = 1.0 - pow(P.b1, (double)n);
-    P.sc->bc2 = 1.0 - pow(P.b2, (double)n);
-  }
-  if (P.bgap) {
-    // u_b = hstack(U[0,:], U[-1,:], U[:,0], U[:,-1]) (2D) / u[Xind] (1D); fixed-order sum
-    double acc = 0.0;
-    if (P.dim == 2) {
-      // 8 boundary entries per thread per pass, loads issued before the sums (one round trip
-      // for the usual 4N <= 2048 entries instead of one per entry)
-      const int n1 = P.n1, n2 = P.n2, nb = 2 * n2 + 2 * n1;
-      for (int k0 = t; k0 < nb; k0 += 8 * blockDim.x) {
-        double uu[8], bb[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int k = k0 + r * blockDim.x;
-          const bool ok = k < nb;
-          int i, j;
-          if (k < n2) { i = 0; j = k; }
-          else if (k < 2 * n2) { i = n1 - 1; j = k - n2; }
-          else if (k < 2 * n2 + n1) { i = k - 2 * n2; j = 0; }
-          else { i = k - 2 * n2 - n1; j = n2 - 1; }
-          uu[r] = ok ? P.Up[(size_t)i * P.p2 + j] : 0.0;
-          bb[r] = ok ? P.bvals[k] : 0.0;
-        }
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const double d = uu[r] - bb[r];
-          acc += d * d;
-        }
-      }
-    } else {
-      for (int k = t; k < P.nb; k += blockDim.x) {
-        const double r = P.Up[P.bidx[k]] - P.bvals[k];
-        acc += r * r;
-      }
-    }
-    __shared__ double sb[4];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((t & 63) == 0) sb[t >> 6] = acc;
-    __syncthreads();
-    if (t == 0) *P.bgap = (sb[0] + sb[1]) + (sb[2] + sb[3]);
-  }
-}
 
 // Pivot block 0 (rows/cols 0..31) of the SPD inverse, factored inside the assembly launch by
 // one extra workgroup per axis.  The 16 workgroups that assemble tile (0,0) release their rows

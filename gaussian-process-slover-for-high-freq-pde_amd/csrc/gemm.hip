@@ -201,8 +201,108 @@ __device__ __forceinline__ d4 mma_chunk(const double* __restrict__ A, int lda, i
   return acc;
 }
 
-__global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
-                                                         const StepScalars* __restrict__ sc) {
+// Operands whose contiguous dimension is k (A untransposed, B transposed) read as MFMA
+// fragments directly would touch 16 rows x 32 B per load instruction (16 cache lines for 512
+// useful bytes, 16 instructions per 64-deep block).  Instead each wave loads its 16 x 64 block
+// with 8 coalesced 16-B loads per lane (2 whole 512-B rows per instruction), stages it in its
+// own LDS block and reads the fragments back (row stride FS = 66 doubles: the 32 lanes of each
+// ds_read_b64 half hit 64 distinct banks).
+constexpr int FS = 66;
+__device__ __forceinline__ void rowblk_load(const double* M, int ld, int r0, int k0, int lane,
+                                            double2* g) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    g[q] = *reinterpret_cast<const double2*>(M + (size_t)(r0 + 2 * q + (lane >> 5)) * ld + k0 + 2 * (lane & 31));
+}
+__device__ __forceinline__ void rowblk_frag(double* buf, const double2* g, int lane, double* f) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    *reinterpret_cast<double2*>(buf + (2 * q + (lane >> 5)) * FS + 2 * (lane & 31)) = g[q];
+  // (one wave's LDS operations complete in issue order: the reads see the writes, and the
+  // next block's writes land after these reads -- no wait or barrier needed)
+#pragma unroll
+  for (int s = 0; s < 16; ++s) f[s] = buf[(lane & 15) * FS + 4 * s + (lane >> 4)];
+}
+
+// One 64-deep block of op(A) op(B) [+ op(A2) op(B2)] for this wave's 16x16 tile: fragments of
+// the k-contiguous operands through LDS (above), the others loaded directly (already coalesced:
+// 16 consecutive doubles of one row per 16 lanes); every global load of both products issued
+// before the first MFMA.  The staging pattern is a template (SA = A untransposed, SB = B
+// transposed): with runtime-selected arrays LLVM kept the operand arrays in scratch.
+template <bool K>  // K: k-contiguous rows r0.. (staged) ; else direct fragment loads
+__device__ __forceinline__ void frag_issue(const double* M, int ld, int r0, int k0, int lane,
+                                           double2 (&g)[8], double (&f)[16]) {
+  if constexpr (K) {
+    rowblk_load(M, ld, r0, k0, lane, g);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) f[s] = M[(size_t)(k0 + 4 * s + (lane >> 4)) * ld + r0 + (lane & 15)];
+  }
+}
+template <bool SA1, bool SB1, bool SA2, bool SB2, bool DUAL>
+__device__ __forceinline__ void blk64(const GemmDesc& d, int i0, int j0, int b0, int c0, int lane,
+                                      double* bufA, double* bufB, d4& acc1, d4& acc2) {
+  double2 ga1[8], gb1[8], ga2[8], gb2[8];
+  double a1[16], bb1[16], a2[16], bb2[16];
+  frag_issue<SA1>(d.A, d.lda, i0, b0, lane, ga1, a1);
+  frag_issue<SB1>(d.B, d.ldb, j0, b0, lane, gb1, bb1);
+  if constexpr (DUAL) {
+    frag_issue<SA2>(d.A2, d.lda2, i0, c0, lane, ga2, a2);
+    frag_issue<SB2>(d.B2, d.ldb2, j0, c0, lane, gb2, bb2);
+  }
+  if constexpr (SA1) rowblk_frag(bufA, ga1, lane, a1);
+  if constexpr (SB1) rowblk_frag(bufB, gb1, lane, bb1);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], bb1[s], acc1, 0, 0, 0);
+  if constexpr (DUAL) {
+    if constexpr (SA2) rowblk_frag(bufA, ga2, lane, a2);
+    if constexpr (SB2) rowblk_frag(bufB, gb2, lane, bb2);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s], bb2[s], acc2, 0, 0, 0);
+  }
+}
+// runtime transpose flags -> one of the 4 (single) / 16 (dual) instantiations (uniform branch)
+__device__ __forceinline__ void blk64_dispatch(const GemmDesc& d, int i0, int j0, int b0, int c0,
+                                               int lane, double* bufA, double* bufB, d4& acc1,
+                                               d4& acc2) {
+  const int code = (!d.ta) | (d.tb << 1) | ((!d.ta2) << 2) | (d.tb2 << 3);
+#define GPK_B64(c) blk64<((c) & 1) != 0, ((c) & 2) != 0, ((c) & 4) != 0, ((c) & 8) != 0, true>
+#define GPK_B64S(c) blk64<((c) & 1) != 0, ((c) & 2) != 0, false, false, false>
+  if (d.K2) {
+    switch (code) {
+      case 0: GPK_B64(0)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 1: GPK_B64(1)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 2: GPK_B64(2)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 3: GPK_B64(3)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 4: GPK_B64(4)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 5: GPK_B64(5)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 6: GPK_B64(6)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 7: GPK_B64(7)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 8: GPK_B64(8)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 9: GPK_B64(9)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 10: GPK_B64(10)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 11: GPK_B64(11)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 12: GPK_B64(12)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 13: GPK_B64(13)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 14: GPK_B64(14)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      default: GPK_B64(15)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+    }
+  } else {
+    switch (code & 3) {
+      case 0: GPK_B64S(0)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 1: GPK_B64S(1)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      case 2: GPK_B64S(2)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+      default: GPK_B64S(3)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
+    }
+  }
+#undef GPK_B64
+#undef GPK_B64S
+}
+
+// waves_per_eu(2): 256 VGPRs per lane (two workgroups per CU), enough for both products'
+// staged operands in flight without spilling them to scratch
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_small_kernel(
+    GemmBatch batch, const StepScalars* __restrict__ sc) {
   const GemmDesc& d = batch.d[blockIdx.y];
   const int tn = d.N >> 4;
   const int tiles = (d.M >> 4) * tn;
@@ -211,7 +311,9 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
   // closed gate ends the workgroup before any operand load (launch + one round trip)
   const bool open = gate_open(d.gate);
   const int i0 = (blockIdx.x / tn) * 16, j0 = (blockIdx.x % tn) * 16;
-  __shared__ double part[2][4][256];
+  // per-wave operand staging (2 blocks of 16 x FS), reused for the cross-wave partial sums
+  __shared__ double smem[4 * 2 * 16 * FS];
+  double(*part)[4][256] = reinterpret_cast<double(*)[4][256]>(smem);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   [[maybe_unused]] const int tslot = SLOT_GEMM + 4 * (d.tag & 15);
   if (TR_FIRST) TR_LO(tslot);
@@ -229,14 +331,21 @@ __global__ __launch_bounds__(256) void gemm_small_kernel(GemmBatch batch,
     for (int r = 0; r < 4; ++r) ein[r] = epi_fetch(d, i0 + (lane >> 4) + 4 * r, j0 + (lane & 15));
   }
   if (!open) return;  // uniform
-  int b0, b1;
+  int b0, b1, c0 = 0, c1 = 0;
   range(d.K, b0, b1);
+  if (d.K2) range(d.K2, c0, c1);
   d4 acc1 = {0.0, 0.0, 0.0, 0.0}, acc2 = {0.0, 0.0, 0.0, 0.0};
-  acc1 = mma_chunk(d.A, d.lda, d.ta, d.B, d.ldb, d.tb, i0, j0, b0, b1, lane, acc1);
-  if (d.K2) {
-    range(d.K2, b0, b1);
-    acc2 = mma_chunk(d.A2, d.lda2, d.ta2, d.B2, d.ldb2, d.tb2, i0, j0, b0, b1, lane, acc2);
+  if (b1 - b0 == 64 && (!d.K2 || c1 - c0 == 64)) {
+    // one 64-deep block per wave and product (K = 256): every global operand load of both
+    // products in flight before the first MFMA (one memory round trip)
+    double* bufA = smem + wv * 2 * 16 * FS;
+    double* bufB = bufA + 16 * FS;
+    blk64_dispatch(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2);
+  } else {  // (per wave: with K = 224 wave 0 takes 32 deep, the others 64)
+    acc1 = mma_chunk(d.A, d.lda, d.ta, d.B, d.ldb, d.tb, i0, j0, b0, b1, lane, acc1);
+    if (d.K2) acc2 = mma_chunk(d.A2, d.lda2, d.ta2, d.B2, d.ldb2, d.tb2, i0, j0, c0, c1, lane, acc2);
   }
+  __syncthreads();  // every wave done with its staging block before `part` reuses the LDS
   if (TR_FIRST) TR_HI(tslot + 2);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {

@@ -225,7 +225,8 @@ static void fill_spd(gpk_handle* h, SpdArgs* sa) {
 }
 
 // the persistent small-factor inverse; gather: K (+ Kc, D) straight from the distance classes
-static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin, bool aug = true) {
+static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin, bool aug = true,
+                               const PrepArgs* prep = nullptr) {
   const Layout& L = h->L;
   ChainArgs ca[2] = {};
   for (int a = 0; a < L.naxes; ++a) {
@@ -249,7 +250,7 @@ static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin, bool au
     }
     fin[a] = h->K[a];
   }
-  return launch_spd_chain(ca, L.naxes, h->prob.eq == GPK_ADVECTION ? 1 : 2, h->s);
+  return launch_spd_chain(ca, L.naxes, h->prob.eq == GPK_ADVECTION ? 1 : 2, h->s, prep, L.q);
 }
 
 // the SPD inverse of every factor (small: 32-wide sweeps, pivot 0 possibly fused into the
@@ -284,16 +285,19 @@ static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
       aa[a].flag = h->aflag[a];
     }
   }
-  // chain + classes: the class values only; the inverse launch gathers K, Kc, D itself
+  // chain + classes: the class values only; the inverse launch gathers K, Kc, D itself and
+  // publishes the step constants from one extra workgroup (off the critical path)
   const bool eval_only = h->chain && h->cls[0].ncls > 0;
-  TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, apply), h->s, eval_only),
+  PrepArgs prep = make_prep(h, apply), prep_eval = prep;
+  prep_eval.skip = eval_only ? 1 : 0;
+  TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, prep_eval, h->s, eval_only),
                    "assemble"));
   mark(h, 1);
   SpdArgs sa[2];
   fill_spd(h, sa);
   double* fin[2] = {nullptr, nullptr};
   if (h->chain)
-    TRY(check_launch(launch_chain(h, eval_only, fin), "spd_chain"));
+    TRY(check_launch(launch_chain(h, eval_only, fin, true, eval_only ? &prep : nullptr), "spd_chain"));
   else
     TRY(check_launch(launch_inverse(h, sa, fin, true), "spd_inverse"));
   for (int a = 0; a < L.naxes; ++a) h->Kinv[a] = fin[a];

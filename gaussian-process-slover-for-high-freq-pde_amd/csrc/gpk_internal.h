@@ -99,6 +99,7 @@ struct PrepArgs {
   const double* Up; const double* bvals; const int* bidx;
   int nb, dim, n1, n2, p2;
   double* bgap;        // out [1]
+  int skip;            // 1: this launch does not publish them (another launch of the step does)
 };
 
 // Distance classes.  Every field of a stationary kernel depends on the pair (i, j) only
@@ -192,7 +193,9 @@ struct ChainArgs {
   double* PBa; int ldpba;                  // augmented panel buffer [p][32*(tu+td)]
 };
 int spd_chain_blocks(const int* p, int nmat, bool aug);
-hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s);
+// prep (nullable): the step constants are published by one extra workgroup of this launch
+hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s,
+                            const PrepArgs* prep = nullptr, int q = 0);
 
 // Large-factor path (spdinv_big.hip): 64-wide pivots, panel + lower-tile MFMA update per sweep,
 // next pivot factored inside the update launch.  In place: K^{-1} ends in X.  Y is used as the

@@ -26,6 +26,7 @@
 #include "gpk_internal.h"
 #include "spd_pivot.h"
 #include "gpk_trace.h"
+#include "prep_dev.h"
 
 namespace gpk {
 
@@ -228,6 +229,9 @@ struct ChainFactor {
 };
 struct ChainBatch {
   ChainFactor f[2];
+  int nmat;
+  PrepArgs prep;  // published by workgroup (0, nmat) when the grid has that extra row
+  int q;
 };
 
 __device__ __forceinline__ void st_sc1(double* p, double v) {
@@ -250,6 +254,10 @@ __device__ __forceinline__ void signal_flag(unsigned int* f) {
 template <int DERIV, bool GATHER>
 __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   const int m = blockIdx.y;
+  if (m == b.nmat) {  // the step constants, off the inverse's critical path
+    if (blockIdx.x == 0) publish_prep(b.prep, b.q);
+    return;
+  }
   const ChainFactor& F = b.f[m];
   const int T = F.T, p = F.p;
   const int TC = T + F.tu + F.td;  // tile columns: K, then the augmented B_u, D^T columns
@@ -459,8 +467,14 @@ int spd_chain_blocks(const int* p, int nmat, bool aug) {
   return blocks;
 }
 
-hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s) {
+hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s,
+                            const PrepArgs* prep, int q) {
   ChainBatch b{};
+  b.nmat = nmat;
+  if (prep) {
+    b.prep = *prep;
+    b.q = q;
+  }
   int Tmax = 0;
   bool gather = a[0].cid != nullptr;
   for (int m = 0; m < nmat; ++m) {
@@ -475,7 +489,7 @@ hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t
     if ((a[m].cid != nullptr) != gather) return hipErrorInvalidValue;
     Tmax = std::max(Tmax, f.T * (f.T + f.tu + f.td));
   }
-  dim3 grid(Tmax, nmat);
+  dim3 grid(Tmax, nmat + (prep ? 1 : 0));
   if (!gather)
     hipLaunchKernelGGL((chain_kernel<0, false>), grid, dim3(256), 0, s, b);
   else if (deriv == 1)
