@@ -1119,7 +1119,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     A_(h->Kc[a], (size_t)P * P);
     A_(h->pst[a], 2);
     A_(h->aflag[a], 1);
-    A_(h->cflags[a], (size_t)(P / 32) * (P / 32 + (P1 + P2) / 32) + P / 32 + 1);
+    A_(h->cflags[a], (size_t)(P / 32) * (P / 32 + (P1 + P2) / 32) + 2 * (P / 32) + 1);
     if (h->chain_aug) {
       A_(h->PD[a], (size_t)P * P);
       A_(h->PBa[a], (size_t)P * (P1 + P2));

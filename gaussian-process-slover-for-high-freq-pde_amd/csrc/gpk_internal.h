@@ -182,7 +182,7 @@ hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
 constexpr int CHAIN_MAX_BLOCKS = 512;
 struct ChainArgs {
   double* X; double* PB; double* piv; double* ldet; double* pst; int* status;
-  unsigned int* flags;  // [T*(T+tu+td) + T + 1], zero-initialised
+  unsigned int* flags;  // [T*(T+tu+td) + 2T + 1], zero-initialised
   int p, n;
   const int* cid; const double* kval; const double* dval; const double* x; double jitter;
   double* Kc; double* D;

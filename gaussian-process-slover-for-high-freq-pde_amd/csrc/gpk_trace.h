@@ -20,7 +20,7 @@ enum TraceSlot {
   SLOT_PG_TOP = 44, SLOT_PG_UPLANE = 45, SLOT_PG_FINAL = 46,
   // dispatch spread (last workgroup start) and intermediate points
   SLOT_PG_START = 47, SLOT_PG_STAGED = 48, SLOT_CSUM_START = 49, SLOT_CEVAL_START = 50,
-  SLOT_GATHER_START = 51, SLOT_CSUM_LOADED = 52,
+  SLOT_GATHER_START = 51, SLOT_CSUM_LOADED = 52, SLOT_CHAIN_END = 53, SLOT_CHAIN_M1 = 54,
   SLOT_GEMM = 64,  // + 4 * stage: first wg [start, end], + 1: first wg operands loaded,
                    // + 2: first wg MFMAs done, + 3: last wg [start, end]  (stages < 16)
 };

@@ -40,8 +40,18 @@ __device__ __forceinline__ double rsqrt_f64(double p) {
 // LP: the LDS pointer type -- plain double* when inlined into a kernel (address space inferred),
 // lds_ptr (address_space(3)) when called through a non-inlined function, so that the callee
 // still issues ds_read / ds_write instead of flat memory instructions.
-template <int BS = 4, typename LP = double*>
-__device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t, int* status) {
+// Hook (optional): hook.early() runs in every thread before the barrier that ends block step 1,
+// hook.pre() before the one that ends step 4 and hook.post() right after it -- a window to poll
+// (without waiting) for the NEXT pivot's inputs and start their loads while this factorisation
+// still has 3 block steps to go (chain_kernel's pivot chain).
+struct NoPivotHook {
+  __device__ void early() {}
+  __device__ void pre() {}
+  __device__ void post() {}
+};
+template <int BS = 4, typename LP = double*, typename Hook = NoPivotHook>
+__device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t, int* status,
+                                                       Hook hook = Hook()) {
   static_assert(BS == 4, "the MFMA update is rank 4");
   typedef double dv4 __attribute__((ext_vector_type(4)));
   const int lane = t & 63, wv = t >> 6, wr = wv >> 1, wc = wv & 1;
@@ -126,7 +136,10 @@ __device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t,
         M[row * SP + cj] = accM[r];
       }
     }
+    if (kb == 1) hook.early();
+    if (kb == 4) hook.pre();
     __syncthreads();
+    if (kb == 4) hook.post();
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) M[(16 * wr + lk + 4 * r) * SP + cj] = accM[r];

@@ -251,6 +251,18 @@ __device__ __forceinline__ void signal_flag(unsigned int* f) {
   if (threadIdx.x == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// the pivot chain's inputs for pivot k+1: panel tile (k, k+1) (LDS-staging layout) and the
+// diagonal tile (k+1, k+1) (MFMA quadrant layout), both after sweep k-1, sc1 loads
+__device__ __forceinline__ void load_inputs(const ChainFactor* F, double* xpre, double* dpre, int k,
+                                            int p, int tx, int ty, int wr, int wc, int lane) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    xpre[r] = ld_sc1(F->PB + (size_t)(k * 32 + ty + 8 * r) * p + (k + 1) * 32 + tx);
+    dpre[r] = ld_sc1(F->PB + (size_t)((k + 1) * 32 + 16 * wr + (lane >> 4) + 4 * r) * p + (k + 1) * 32 +
+                     16 * wc + (lane & 15));  // the diagonal tile's slot
+  }
+}
+
 template <int DERIV, bool GATHER>
 __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   const int m = blockIdx.y;
@@ -262,8 +274,9 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   const int T = F.T, p = F.p;
   const int TC = T + F.tu + F.td;  // tile columns: K, then the augmented B_u, D^T columns
   const int tile = blockIdx.x;
-  if (tile >= T * TC) return;
-  const int I = tile / TC, J = tile % TC;
+  if (tile > T * TC) return;
+  const bool master = tile == T * TC;  // the pivot chain's own workgroup (below)
+  const int I = master ? 0 : tile / TC, J = master ? 0 : tile % TC;
   const bool aug = J >= T;
   const int ja = J - T;  // augmented tile column
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -271,7 +284,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   const int tx = t & 31, ty = t >> 5;
   unsigned int* panel_rdy = F.flags;
   unsigned int* piv_rdy = F.flags + T * TC;
-  unsigned int* done = F.flags + T * TC + T;
+  unsigned int* diag_rdy = F.flags + T * TC + T;
+  unsigned int* done = F.flags + T * TC + 2 * T;
   // panel tile (row k) of column J: K part in PB, augmented part in PBa
   auto panel_ptr = [&](int k, int row, int col) -> double* {
     return J < T ? F.PB + (size_t)(k * 32 + row) * p + J * 32 + col
@@ -318,8 +332,10 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
         kv = (i == j) ? 1.0 : 0.0;
         dv = 0.0;
       }
-      if (F.Kc) F.Kc[o] = kv;
-      if (DERIV) F.D[o] = dv;
+      if (!master) {
+        if (F.Kc) F.Kc[o] = kv;
+        if (DERIV) F.D[o] = dv;
+      }
       acc[r] = kv;
     } else {
       acc[r] = F.X[o];
@@ -330,41 +346,104 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     for (int r = 0; r < 4; ++r) st_sc1(panel_ptr(I, 16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15)), acc[r]);
     signal_flag(panel_rdy + I * TC + J);
   };
-  const bool trm = t == 0 && m == 0;  // probes (gpk_trace.h): factor 0's pivot owners
-  auto factor_pivot = [&](int kp, bool with_tile) {  // acc: Schur complement of pivot block kp
-    store_quad(sP, SP, wr, wc, lane, acc);
-    __syncthreads();
-    if (with_tile) {  // this tile as the panel of sweep kp (its stores drain with the pivot's)
+  // diagonal tile (I, I) as it is after sweep I-2, for the pivot chain's workgroup: stored in
+  // its own panel slot (I, I) of PB, which the panel of sweep I overwrites only after the chain
+  // has consumed it (that publication needs pivot I, which needs this tile)
+  auto publish_diag = [&](void) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) st_sc1(panel_ptr(I, 16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15)), acc[r]);
-    }
-    if (trm && kp > 0 && kp < 17) TR_LO(SLOT_SWEEP_PIVOT + kp - 1);
-    if (trm && kp == 0) TR_LO(SLOT_PIVOT0);
-    const double ls = pivot_chol_inv_block(sP, sM, pv, t, F.status);
-    for (int e = t; e < 1024; e += 256) st_sc1(F.piv + (size_t)kp * 1024 + e, sM[(e >> 5) * SP + (e & 31)]);
-    if (t == 0) F.ldet[kp] = ls;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-      if (with_tile) __hip_atomic_store(panel_rdy + I * TC + J, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(piv_rdy + kp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP_PIVOT + kp - 1);
-    if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP + kp - 1);
-    if (trm && kp == 0) TR_HI(SLOT_PIVOT0);
+    for (int r = 0; r < 4; ++r) st_sc1(panel_ptr(I, 16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15)), acc[r]);
+    signal_flag(diag_rdy + I);
   };
-  if (trm && tile == 0) TR_LO(SLOT_GATHER);
-  if (I == 0 && J == 0) {
-    if (t == 0) {
+  const bool trm = t == 0 && m == 0;  // probes (gpk_trace.h): factor 0's pivot owners
+  if (master) {
+    // (issue priority over the tile workgroup that may share its CU: this one is the chain)
+    __builtin_amdgcn_s_setprio(3);
+    // The pivot chain, kept in one workgroup: after factoring pivot k it holds L_k^{-1} in LDS,
+    // so pivot k+1's Schur complement X_{k+1,k+1} - V^T V (V = L_k^{-1} X_{k,k+1}) needs no hop
+    // for L_k^{-1}; its two inputs (the panel tile (k, k+1) and the diagonal tile (k+1, k+1)
+    // after sweep k-1) are published by their owners ~2 us after pivot k-1, i.e. while this
+    // workgroup is still factoring pivot k.  Same operations as the owner's update of that tile:
+    // bitwise equal.
+    // the inputs of step k (pivot k+1) are produced while pivot k is being factored: poll for
+    // them and start their loads inside that factorisation (PivotPrefetch), so they are in
+    // registers when it ends
+    double xpre[4], dpre[4];
+    __shared__ int s_pre;  // the prefetch was issued inside the factorisation
+    struct PivotPrefetch {
+      const ChainFactor* F; unsigned int *panel_rdy, *diag_rdy;
+      double *xpre, *dpre;
+      int* s_pre;
+      int k, T, TC, p, t, tx, ty, wr, wc, lane;
+      unsigned int f1, f2;
+      __device__ void early() {  // issue the flag loads; their values are looked at 3 steps later
+        f1 = f2 = 0u;
+        if (k + 1 < T && t == 0) {
+          f1 = __hip_atomic_load(panel_rdy + k * TC + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          f2 = __hip_atomic_load(diag_rdy + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      __device__ void pre() {
+        if (t == 0) *s_pre = (k + 1 < T && f1 != 0u && f2 != 0u) ? 1 : 0;
+      }
+      __device__ void post() {  // both inputs published: load them (sc1) behind the barrier
+        if (!*s_pre) return;
+        load_inputs(F, xpre, dpre, k, p, tx, ty, wr, wc, lane);
+      }
+    };
+    auto factor = [&](int kp) {
+      if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP + kp - 1);  // (inputs in: the hop ends)
+      store_quad(sP, SP, wr, wc, lane, acc);
+      __syncthreads();
+      if (trm && kp > 0 && kp < 17) TR_LO(SLOT_SWEEP_PIVOT + kp - 1);
+      if (trm && kp == 0) TR_LO(SLOT_PIVOT0);
+      PivotPrefetch hook{&F, panel_rdy, diag_rdy, xpre, dpre, &s_pre, kp, T, TC, p, t, tx, ty, wr, wc,
+                         lane, 0u, 0u};
+      const double ls = pivot_chol_inv_block<4, double*, PivotPrefetch>(sP, sM, pv, t, F.status, hook);
+      for (int e = t; e < 1024; e += 256) st_sc1(F.piv + (size_t)kp * 1024 + e, sM[(e >> 5) * SP + (e & 31)]);
+      if (t == 0) F.ldet[kp] = ls;
+      signal_flag(piv_rdy + kp);
+      if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP_PIVOT + kp - 1);
+      if (trm && kp == 0) TR_HI(SLOT_PIVOT0);
+    };
+    factor(0);  // acc = tile (0, 0) of K, gathered above
+    for (int k = 0; k + 1 < T; ++k) {
+      if (!s_pre) {  // (uniform) not yet published at the prefetch point: wait and load now
+        if (t == 0) {
+          wait_flag(panel_rdy + k * TC + k + 1);
+          wait_flag(diag_rdy + k + 1);
+        }
+        __syncthreads();
+        load_inputs(&F, xpre, dpre, k, p, tx, ty, wr, wc, lane);
+      }
+      if (trm && k < 16) TR_LO(SLOT_SWEEP + k);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // prefetched during pivot k's factorisation
+        sXJ[(ty + 8 * r) * SB + tx] = xpre[r];
+        acc[r] = dpre[r];
+      }
+      __syncthreads();
+      d4 vj = {0.0, 0.0, 0.0, 0.0};
+      vj = mma_t(sM, SP, 1, sXJ, SB, 1, wr, wc, lane, vj);  // V = L_k^{-1} X_{k,k+1}
+      __syncthreads();
+      store_quad(sXJ, SB, wr, wc, lane, vj);
+      __syncthreads();
+      d4 prod = {0.0, 0.0, 0.0, 0.0};
+      prod = mma_t(sXJ, 1, SB, sXJ, SB, 1, wr, wc, lane, prod);  // V^T V
+      acc = acc - prod;
+      factor(k + 1);
+    }
+  } else {
+    if (trm && tile == 0) TR_LO(SLOT_GATHER);
+    if (I == 0 && J == 0 && t == 0) {
       F.pst[0] = acc[0];  // K_00 = max diag K (stationary kernel + jitter): refinement gate
       __hip_atomic_store(reinterpret_cast<unsigned long long*>(F.pst + 1), 0ull, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);  // max diag K^{-1}, atomicMax'd at the end
     }
+    if (I == 0 && J != 0) publish_tile();  // row 0 is the panel of sweep 0
+    if (I == 1 && J == 1 && T > 1) publish_diag();  // tile (1, 1) as it is before sweep 0
   }
-  if (I == 0 && J == 0) factor_pivot(0, true);  // row 0 is the panel of sweep 0
-  else if (I == 0) publish_tile();
 
-  for (int k = 0; k < T; ++k) {
+  for (int k = 0; k < T && !master; ++k) {
     const bool needI = I != k, needJ = J != k && J != I;
     // the panel tiles are usually published long before the pivot: fetch them first, then
     // wait for L^{-1}_k
@@ -380,10 +459,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
       xi[r] = needI ? ld_sc1(F.PB + (size_t)(k * 32 + row) * p + I * 32 + tx) : 0.0;
       xj[r] = needJ ? ld_sc1(panel_ptr(k, row, tx)) : 0.0;
     }
-    if (t == 0) {
-      wait_flag(piv_rdy + k);
-      if (trm && I == k + 1 && J == k + 1 && k < 16) TR_LO(SLOT_SWEEP + k);
-    }
+    if (t == 0) wait_flag(piv_rdy + k);
     __syncthreads();
     const double* Li = F.piv + (size_t)k * 1024;
 #pragma unroll
@@ -414,16 +490,13 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
       prod = mma_t(sXI, 1, SB, sVJ, SB, 1, wr, wc, lane, prod); // V_I^T V_J
       acc = acc - prod;
     }
-    if (k + 1 < T && I == k + 1 && J == k + 1) {
-      // the next pivot's owner: its panel tile is needed only with the pivot, so both are
-      // published behind one drain after the factorisation
-      factor_pivot(k + 1, true);
-    } else if (k + 1 < T && I == k + 1) {
-      publish_tile();  // panel of sweep k + 1
-    }
+    // panel of sweep k + 1 (the diagonal tile's panel slot is the pivot chain's: nobody reads
+    // a (k, k) panel tile)
+    if (k + 1 < T && I == k + 1 && J != I) publish_tile();
+    if (I == J && I == k + 2) publish_diag();  // tile (k+2, k+2) after sweep k, for pivot k + 2
     __syncthreads();  // LDS is refilled next sweep
   }
-  if (aug) {  // upper-right block: +K^{-1} B (B_u part possibly stored transposed)
+  if (aug && !master) {  // upper-right block: +K^{-1} B (B_u part possibly stored transposed)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = I * 32 + 16 * wr + (lane >> 4) + 4 * r, jl = ja * 32 + 16 * wc + (lane & 15);
@@ -437,24 +510,27 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   }
   // K^{-1} = -X after the last sweep
 #pragma unroll
-  for (int r = 0; r < 4 && !aug; ++r) {
+  for (int r = 0; r < 4 && !aug && !master; ++r) {
     const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
     const double y = -acc[r];
     F.X[(size_t)(I * 32 + row) * p + J * 32 + col] = y;
     if (I == J && row == col) pv[row] = (I * 32 + row < F.n) ? y : 0.0;
   }
   __syncthreads();
-  if (I == J && t == 0) {  // refinement gate: max_i (K^{-1})_ii of this block
+  if (I == J && t == 0 && !master) {  // refinement gate: max_i (K^{-1})_ii of this block
     double mx = 0.0;
     for (int j = 0; j < 32; ++j) mx = fmax(mx, pv[j]);
     atomicMax(reinterpret_cast<unsigned long long*>(F.pst + 1), (unsigned long long)__double_as_longlong(mx));
   }
   if (trm && tile == 0) TR_HI(SLOT_GATHER);
   // the last workgroup of this factor re-arms the flags for the next launch
-  if (t == 0) s_last = atomicAdd(done, 1u) == (unsigned)(T * TC - 1);
+  if (t == 0 && master && m == 1) TR_HI(SLOT_CHAIN_M1);
+  if (t == 0 && master && m == 1) TR_LO(SLOT_CHAIN_M1);
+  if (t == 0) s_last = atomicAdd(done, 1u) == (unsigned)(T * TC);  // T*TC tiles + the chain
   __syncthreads();
+  if (s_last && t == 0) TR_HI(SLOT_CHAIN_END);
   if (s_last) {
-    for (int e = t; e < T * TC + T; e += 256)
+    for (int e = t; e < T * TC + 2 * T; e += 256)
       __hip_atomic_store(F.flags + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -463,7 +539,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
 int spd_chain_blocks(const int* p, int nmat, bool aug) {
   int blocks = 0, cols = 0;
   for (int m = 0; m < nmat; ++m) cols += p[m] / 32;
-  for (int m = 0; m < nmat; ++m) blocks += (p[m] / 32) * (p[m] / 32 + (aug ? cols : 0));
+  for (int m = 0; m < nmat; ++m) blocks += (p[m] / 32) * (p[m] / 32 + (aug ? cols : 0)) + 1;
   return blocks;
 }
 
@@ -487,7 +563,7 @@ hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t
     f.Ou = a[m].Ou; f.ldou = a[m].ldou; f.ou_t = a[m].ou_t; f.Od = a[m].Od; f.ldod = a[m].ldod;
     f.PBa = a[m].PBa; f.ldpba = a[m].ldpba;
     if ((a[m].cid != nullptr) != gather) return hipErrorInvalidValue;
-    Tmax = std::max(Tmax, f.T * (f.T + f.tu + f.td));
+    Tmax = std::max(Tmax, f.T * (f.T + f.tu + f.td) + 1);  // + the pivot chain's workgroup
   }
   dim3 grid(Tmax, nmat + (prep ? 1 : 0));
   if (!gather)

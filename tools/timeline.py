@@ -19,7 +19,8 @@ NAMES = {0: "class_eval first wg", 1: "gather pivot wg | chain wg(0,0)", 2: "piv
          40: "class_sum first wg", 41: "pgrad first wg start", 42: "pg first wg contracted",
          43: "pg group tails", 44: "pg top tail", 45: "pg U plane wg0", 46: "pg finalize",
          47: "pg last grad wg", 48: "pg first wg staged", 49: "class_sum last wg",
-         50: "class_eval last wg", 51: "gather last wg", 52: "class_sum wg0 loaded"}
+         50: "class_eval last wg", 51: "gather last wg", 52: "class_sum wg0 loaded", 53: "chain: last wg done",
+         54: "chain: factor-1 pivot chain done"}
 for k in range(16):
     NAMES[64 + 4 * k] = f"gemm stage {k} first wg"
     NAMES[65 + 4 * k] = f"  gemm {k} first wg loaded"
@@ -61,4 +62,4 @@ print(f"{a.config}: one step, device timeline (us, mean of {a.steps})")
 for i in sorted(range(128), key=lambda i: (acc_lo[i] / max(cnt[i], 1)) if cnt[i] and not np.isnan(acc_lo[i]) else 1e9):
     if cnt[i]:
         l, h = acc_lo[i] / cnt[i], acc_hi[i] / cnt[i]
-        print(f"  {NAMES.get(i, i):24s} {l:9.2f} .. {h:9.2f}   ({h - l:7.2f})")
+        print(f"  {str(NAMES.get(i, i)):24s} {l:9.2f} .. {h:9.2f}   ({h - l:7.2f})")
