@@ -1176,7 +1176,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   }
   A_(h->pgpart, (size_t)L.naxes * h->bpa * 3 * QMAX);
   A_(h->pg, (size_t)L.naxes * 3 * QMAX);
-  h->ttg = std::max(32, (int)std::ceil(std::sqrt((double)h->bpa)));
+  h->ttg = std::max(16, (int)std::ceil(std::sqrt((double)h->bpa)));  // one 16-load batch per level at C4
   h->tngpa = (h->bpa + h->ttg - 1) / h->ttg;
   A_(h->tcount, (size_t)L.naxes * h->tngpa);
   A_(h->ttop, 1);

@@ -18,16 +18,19 @@
 #include <algorithm>
 
 #include "gpk_internal.h"
-#include "stepk_dev.h"
 #include "gpk_trace.h"
+
+namespace gpk {
+GPK_TRACE_TU(pgrad)
+}  // namespace gpk
+#define FIN_PROBE(slot) TR_HI(slot)  // finalize_body phases (gpk_trace.h)
+#include "stepk_dev.h"
 
 #ifndef GPK_PG_PAIRS
 #define GPK_PG_PAIRS 64
 #endif
 
 namespace gpk {
-
-GPK_TRACE_TU(pgrad)
 
 constexpr int PAIRS = GPK_PG_PAIRS;  // pairs per workgroup (PAIRS/32 rows x 32 cols of a 32x32 tile)
 constexpr int PG_SUB = 1024 / PAIRS;  // workgroups per tile
@@ -79,7 +82,14 @@ __device__ __forceinline__ double strided_sum(const double* p, int stride, int n
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc += v[j];
   }
-  for (; k < n; ++k) acc += ld_wt(p + (size_t)k * stride);
+  if (k < n) {  // remainder: one masked batch (a scalar loop here ran one round trip per load)
+    double v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = ld_wt(p + (size_t)(k + j < n ? k + j : k) * stride);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (k + j < n) acc += v[j];
+  }
   return acc;
 }
 
@@ -103,16 +113,17 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
   if (t == 0) TR_HI(SLOT_PG_GROUP);
   if (!arrive_last(T.top, (unsigned)(b.naxes * T.ngpa), &s_last)) return;
   if (t == 0) TR_LO(SLOT_PG_TOP);
-  for (int e = t; e < b.naxes * 3 * QMAX; e += 256) {
-    const int ax = e / (3 * QMAX), x = e % (3 * QMAX);
-    double acc = 0.0;
-    if ((x % QMAX) < q) acc = strided_sum(T.gpart + (size_t)ax * T.ngpa * (3 * QMAX) + x, 3 * QMAX, T.ngpa);
-    T.pg[e] = acc;
+  // only the naxes * 3q live entries (<= 256 at Q <= 42: one batch of loads per thread; a loop
+  // over all 3 QMAX slots per axis ran two dependent batches in half the threads)
+  for (int e = t; e < b.naxes * 3 * q; e += 256) {
+    const int ax = e / (3 * q), rem = e % (3 * q);
+    const int x = (rem / q) * QMAX + rem % q;
+    T.pg[ax * 3 * QMAX + x] = strided_sum(T.gpart + (size_t)ax * T.ngpa * (3 * QMAX) + x, 3 * QMAX, T.ngpa);
   }
   __syncthreads();  // pg (global) written by this block is visible to it after the barrier
   if (t == 0) *T.top = 0u;
   if (t == 0) TR_HI(SLOT_PG_TOP);
-  finalize_body(T.fin);
+  finalize_body(T.fin, 2);  // (the loss part ran at the start of the launch)
   if (t == 0) TR_HI(SLOT_PG_FINAL);
 }
 
@@ -245,6 +256,10 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
   const int axis = blockIdx.y;
   const int blk = blockIdx.x;
   if (TR_FIRST) TR_LO(SLOT_PGRAD);
+  if (axis == b.naxes + 1) {  // fused tail: the loss and log_tau / log_v update, off the chain
+    if (blk == 0) finalize_body(b.tail.fin, 1);
+    return;
+  }
   if (axis == b.naxes) {
     if (threadIdx.x == 0 && blk == 0) TR_LO(SLOT_PG_UPLANE);  // fused tail: dL/dU + Adam on U (grid-stride over the solution grid)
     const int nu = tail_nu(b.tail.adam.L);
@@ -430,7 +445,7 @@ static void launch_pg_c(const PGradBatch& b, int naxes, int bpa, int q, int deri
                         const StepScalars* sc, hipStream_t s) {
   // the U plane (dL/dU + Adam) gets one element per thread when it is wider than bpa blocks
   const int ublocks = b.tail.fused ? (tail_nu(b.tail.adam.L) + 255) / 256 : 0;
-  dim3 grid(std::max(bpa, std::min(ublocks, 4096)), naxes + (b.tail.fused ? 1 : 0));
+  dim3 grid(std::max(bpa, std::min(ublocks, 4096)), naxes + (b.tail.fused ? 2 : 0));
   if (mode1d) {
     hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, true, CLS>), grid, dim3(256), 0, s, b, q, sc);
   } else if (deriv == 2) {

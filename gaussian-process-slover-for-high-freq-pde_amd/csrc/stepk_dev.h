@@ -5,6 +5,10 @@
 #include "gpk_internal.h"
 #include "stepk.h"
 
+#ifndef FIN_PROBE
+#define FIN_PROBE(slot) ((void)0)
+#endif
+
 namespace gpk {
 
 __device__ __forceinline__ void adam1(double g, double& p, double& m, double& v, const AdamHyper& h,
@@ -32,7 +36,12 @@ __device__ inline double block_sum(double v, double* sh) {
 // Latency-bound (one workgroup on the step's critical path): every global load it needs is
 // issued up front (one memory round trip), and the small parameters' gradients and Adam updates
 // stay in the registers of the thread that owns them (no store / barrier / reload).
-__device__ inline void finalize_body(const FinalizeArgs& f) {
+// part: 0 = everything; 1 = the loss, the log_tau / log_v gradients and their Adam (needs no
+// kernel-parameter gradient: the fused tail runs it in a workgroup of its own at the start of
+// the launch); 2 = the kernel-parameter gradients from f.pg and their Adam (the tail's last
+// workgroup, right after it has reduced pg).
+__device__ inline void finalize_body(const FinalizeArgs& f, int part = 0) {
+  const bool do_loss = part != 2, do_kp = part != 1;
   __shared__ double sh[4], sld[2], sg[2];
   const int t = threadIdx.x;
   const Layout& L = f.L;
@@ -43,20 +52,24 @@ __device__ inline void finalize_body(const FinalizeArgs& f) {
   const double* lp = ((t >> 6) == 1 && L.naxes > 1) ? f.ldet[1] : f.ldet[0];  // never null
   const int nl = (t >> 6) >= L.naxes ? 0 : (t >> 6) == 1 ? f.nldet[1] : f.nldet[0];
   const int lk = t & 63;
-  const double q0 = f.red_quad[t < f.nquad ? t : 0], e0 = f.red_egap[t < f.negap ? t : 0];
-  const double l0 = lp[lk < nl ? lk : 0];
-  double quad = t < f.nquad ? q0 : 0.0, egap = t < f.negap ? e0 : 0.0;
-  for (int i = t + 256; i < f.nquad; i += 256) quad += f.red_quad[i];
-  for (int i = t + 256; i < f.negap; i += 256) egap += f.red_egap[i];
-  double ldx = (t < 128 && lk < nl) ? l0 : 0.0;  // log det of factor t >> 6: its pivot blocks
-  if (t < 128)
-    for (int k = lk + 64; k < nl; k += 64) ldx += lp[k];
-  const double bgap = *f.bgap;  // boundary gap of U at the start of the step (assembly launch)
+  double quad = 0.0, egap = 0.0, ldx = 0.0, bgap = 0.0;
+  if (do_loss) {  // (uniform)
+    const double q0 = f.red_quad[t < f.nquad ? t : 0], e0 = f.red_egap[t < f.negap ? t : 0];
+    const double l0 = lp[lk < nl ? lk : 0];
+    bgap = *f.bgap;  // boundary gap of U at the start of the step (assembly launch)
+    quad = t < f.nquad ? q0 : 0.0;
+    egap = t < f.negap ? e0 : 0.0;
+    for (int i = t + 256; i < f.nquad; i += 256) quad += f.red_quad[i];
+    for (int i = t + 256; i < f.negap; i += 256) egap += f.red_egap[i];
+    ldx = (t < 128 && lk < nl) ? l0 : 0.0;  // log det of factor t >> 6: its pivot blocks
+    if (t < 128)
+      for (int k = lk + 64; k < nl; k += 64) ldx += lp[k];
+  }
   const double tau = f.sc->tau, v = f.sc->v, bc1 = f.sc->bc1, bc2 = f.sc->bc2;
   const double log_tau = f.params[L.off_tau], log_v = f.params[L.off_v];
   int slot = 0;
   bool gate = false;
-  if (t == 0) {
+  if (t == 0 && do_loss) {
     slot = *f.loss_slot;
     if (f.viol)
       for (int a = 0; a < L.naxes; ++a) gate |= f.watch[a] && gate_open(f.watch[a]);
@@ -78,8 +91,11 @@ __device__ inline void finalize_body(const FinalizeArgs& f) {
     pp[r] = f.params[idx];
     pm[r] = f.m[idx];
     pv2[r] = f.v[idx];
-    if (idx == L.off_tau) { pkind[r] = 1; continue; }
-    if (idx == L.off_v) { pkind[r] = 2; continue; }
+    if (idx == L.off_tau || idx == L.off_v) {
+      pkind[r] = do_loss ? (idx == L.off_tau ? 1 : 2) : -1;
+      continue;
+    }
+    if (!do_kp) continue;
     const int a = (L.naxes == 2 && idx >= L.off_kp[1]) ? 1 : 0;
     const int rr = idx - L.off_kp[a], ty = rr / L.q, c = rr % L.q;  // ty: freq, log-ls, log-w
     pkind[r] = 0;
@@ -87,6 +103,8 @@ __device__ inline void finalize_body(const FinalizeArgs& f) {
     pgx[r] = (ty == 0 && !f.has_cos) ? 0.0 : f.pg[a * 3 * QMAX + ty * QMAX + c];
   }
   // ---- phase 1: reductions, loss (thread 0)
+  if (t == 0) FIN_PROBE(55);
+  if (do_loss) {
   if (t < 128) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ldx += __shfl_xor(ldx, o, 64);
@@ -94,8 +112,10 @@ __device__ inline void finalize_body(const FinalizeArgs& f) {
   }
   quad = block_sum(quad, sh);
   egap = block_sum(egap, sh);  // (its barriers also publish sld)
+  }
+  if (t == 0) FIN_PROBE(56);
   const double wb = f.llk_weight, c = f.logdet;
-  if (t == 0) {
+  if (t == 0 && do_loss) {
     if (gate) atomicOr(f.viol, 1u);
     const double ld[2] = {sld[0], L.naxes > 1 ? sld[1] : 0.0};
     const double Nb = (L.dim == 2) ? (double)(2 * L.n2 + 2 * L.n1) : (double)f.nb;
@@ -116,6 +136,7 @@ __device__ inline void finalize_body(const FinalizeArgs& f) {
     diag[0] = loss; diag[1] = ld[0]; diag[2] = ld[1]; diag[3] = quad; diag[4] = egap; diag[5] = bgap;
   }
   __syncthreads();
+  if (t == 0) FIN_PROBE(57);
   // ---- phase 2: gradients (kernel params: the fields were contracted without the weight w_q)
   // and Adam on the small parameters
 #pragma unroll
