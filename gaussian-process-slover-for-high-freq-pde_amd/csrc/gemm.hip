@@ -262,13 +262,14 @@ __device__ __forceinline__ void blk64(const GemmDesc& d, int i0, int j0, int b0,
   }
 }
 // runtime transpose flags -> one of the 4 (single) / 16 (dual) instantiations (uniform branch)
+template <bool DUAL>
 __device__ __forceinline__ void blk64_dispatch(const GemmDesc& d, int i0, int j0, int b0, int c0,
                                                int lane, double* bufA, double* bufB, d4& acc1,
                                                d4& acc2) {
   const int code = (!d.ta) | (d.tb << 1) | ((!d.ta2) << 2) | (d.tb2 << 3);
 #define GPK_B64(c) blk64<((c) & 1) != 0, ((c) & 2) != 0, ((c) & 4) != 0, ((c) & 8) != 0, true>
 #define GPK_B64S(c) blk64<((c) & 1) != 0, ((c) & 2) != 0, false, false, false>
-  if (d.K2) {
+  if (DUAL && d.K2) {
     switch (code) {
       case 0: GPK_B64(0)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
       case 1: GPK_B64(1)(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2); break;
@@ -299,10 +300,13 @@ __device__ __forceinline__ void blk64_dispatch(const GemmDesc& d, int i0, int j0
 #undef GPK_B64S
 }
 
-// waves_per_eu(2): 256 VGPRs per lane (two workgroups per CU), enough for both products'
-// staged operands in flight without spilling them to scratch
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_small_kernel(
-    GemmBatch batch, const StepScalars* __restrict__ sc) {
+// DUAL (some descriptor has a second product): waves_per_eu(2) = 256 VGPRs per lane, enough for
+// both products' staged operands in flight without spilling.  Batches without one (C4's G_D
+// stage: 4 descriptors = 1024 workgroups) get waves_per_eu(4), four workgroups per CU: one
+// round over the chip instead of two.
+template <bool DUAL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DUAL ? 2 : 4, DUAL ? 2 : 4)))
+void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
   const GemmDesc& d = batch.d[blockIdx.y];
   const int tn = d.N >> 4;
   const int tiles = (d.M >> 4) * tn;
@@ -311,8 +315,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // closed gate ends the workgroup before any operand load (launch + one round trip)
   const bool open = gate_open(d.gate);
   const int i0 = (blockIdx.x / tn) * 16, j0 = (blockIdx.x % tn) * 16;
-  // per-wave operand staging (2 blocks of 16 x FS), reused for the cross-wave partial sums
-  __shared__ double smem[4 * 2 * 16 * FS];
+  // per-wave operand staging (one 16 x FS block, A then B), reused for the cross-wave partials
+  __shared__ double smem[4 * 16 * FS];
   double(*part)[4][256] = reinterpret_cast<double(*)[4][256]>(smem);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   [[maybe_unused]] const int tslot = SLOT_GEMM + 4 * (d.tag & 15);
@@ -333,17 +337,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (!open) return;  // uniform
   int b0, b1, c0 = 0, c1 = 0;
   range(d.K, b0, b1);
-  if (d.K2) range(d.K2, c0, c1);
+  if (DUAL && d.K2) range(d.K2, c0, c1);
   d4 acc1 = {0.0, 0.0, 0.0, 0.0}, acc2 = {0.0, 0.0, 0.0, 0.0};
-  if (b1 - b0 == 64 && (!d.K2 || c1 - c0 == 64)) {
+  if (b1 - b0 == 64 && (!(DUAL && d.K2) || c1 - c0 == 64)) {
     // one 64-deep block per wave and product (K = 256): every global operand load of both
     // products in flight before the first MFMA (one memory round trip)
-    double* bufA = smem + wv * 2 * 16 * FS;
-    double* bufB = bufA + 16 * FS;
-    blk64_dispatch(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2);
+    double* bufA = smem + wv * 16 * FS;
+    double* bufB = bufA;  // (in-order LDS per wave: B's block lands after A's fragments are read)
+    blk64_dispatch<DUAL>(d, i0, j0, b0, c0, lane, bufA, bufB, acc1, acc2);
   } else {  // (per wave: with K = 224 wave 0 takes 32 deep, the others 64)
     acc1 = mma_chunk(d.A, d.lda, d.ta, d.B, d.ldb, d.tb, i0, j0, b0, b1, lane, acc1);
-    if (d.K2) acc2 = mma_chunk(d.A2, d.lda2, d.ta2, d.B2, d.ldb2, d.tb2, i0, j0, c0, c1, lane, acc2);
+    if (DUAL && d.K2) acc2 = mma_chunk(d.A2, d.lda2, d.ta2, d.B2, d.ldb2, d.tb2, i0, j0, c0, c1, lane, acc2);
   }
   __syncthreads();  // every wave done with its staging block before `part` reuses the LDS
   if (TR_FIRST) TR_HI(tslot + 2);
@@ -365,7 +369,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const double s1 = (part[0][0][q] + part[0][1][q]) + (part[0][2][q] + part[0][3][q]);
     const int row = i0 + (lane >> 4) + 4 * r, col = j0 + (lane & 15);
     double c = alpha * s1;
-    if (d.K2) c += alpha2 * ((part[1][0][q] + part[1][1][q]) + (part[1][2][q] + part[1][3][q]));
+    if (DUAL && d.K2) c += alpha2 * ((part[1][0][q] + part[1][1][q]) + (part[1][2][q] + part[1][3][q]));
     d.C[(size_t)row * d.ldc + col] = epi_apply(d, c, ein[r], red, red2);
   }
   if (d.red) {
@@ -381,13 +385,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (TR_FIRST) TR_HI(tslot);
 }
 
+static void launch_small(const GemmBatch& b, int ndesc, int tiles, const StepScalars* sc, hipStream_t s) {
+  bool dual = false;
+  for (int i = 0; i < ndesc; ++i) dual |= b.d[i].K2 != 0;
+  if (dual)
+    hipLaunchKernelGGL(gemm_small_kernel<true>, dim3(tiles, ndesc), dim3(256), 0, s, b, sc);
+  else
+    hipLaunchKernelGGL(gemm_small_kernel<false>, dim3(tiles, ndesc), dim3(256), 0, s, b, sc);
+}
+
 hipError_t launch_gemm_batch(const GemmDesc* descs, int ndesc, int max_tiles,
                              const StepScalars* sc, hipStream_t s, int small) {
   if (ndesc < 1 || ndesc > GEMM_MAX_BATCH) return hipErrorInvalidValue;
   GemmBatch b{};
   for (int i = 0; i < ndesc; ++i) b.d[i] = descs[i];
   if (small)
-    hipLaunchKernelGGL(gemm_small_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, b, sc);
+    launch_small(b, ndesc, max_tiles, sc, s);
   else
     hipLaunchKernelGGL(gemm_kernel, dim3(max_tiles, ndesc), dim3(256), 0, s, b, sc);
   return hipGetLastError();
@@ -819,7 +832,7 @@ hipError_t launch_gemm_auto(const GemmDesc* descs, int ndesc, const StepScalars*
     mt = std::max(mt, gemm_tiles(descs[i], variant));
   }
   if (variant == GEMM_SMALL) {
-    hipLaunchKernelGGL(gemm_small_kernel, dim3(mt, ndesc), dim3(256), 0, s, b, sc);
+    launch_small(b, ndesc, mt, sc, s);
   } else if (variant == GEMM_BIG) {
     const int per = (mt + 7) / 8;
     hipLaunchKernelGGL(gemm_big_kernel, dim3(8 * per, ndesc), dim3(256), 0, s, b, sc, per);
