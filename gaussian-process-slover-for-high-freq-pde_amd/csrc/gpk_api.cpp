@@ -1464,33 +1464,44 @@ static int run_steps(gpk_handle* h, int n_steps, double* losses, bool fast) {
   return GPK_OK;
 }
 
+// Fast batches run in chunks of FAST_CHUNK steps, each checked at its end: a step that met an
+// open refinement gate costs a rerun of its chunk only (not of the whole call -- at C3 the
+// gate opens mid-training, and a 300-step call used to run twice).
+constexpr int FAST_CHUNK = 64;
+
 int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
   if (!h) return fail(GPK_EINVAL, "NULL handle");
   if (n_steps < 0) return fail(GPK_EINVAL, "n_steps < 0");
   DevSwitch ds(h->dev);
-  const bool fast = h->fast_ok && h->fast_mode && n_steps > 0;
-  TRY(capture(h, 1, !fast));
   const size_t np = (size_t)h->L.nparams, nb = np * sizeof(double);
-  if (fast) {  // snapshot of everything a step carries forward (Up is rebuilt from params)
-    HIPCHK(hipMemcpyAsync(h->snap, h->params, nb, hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemcpyAsync(h->snap + np, h->m, nb, hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemcpyAsync(h->snap + 2 * np, h->v, nb, hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemcpyAsync(h->snap_count, h->count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemsetAsync(h->viol, 0, sizeof(unsigned int), h->s));
-  }
-  TRY(run_steps(h, n_steps, losses, fast));
-  bool viol = false;
-  TRY(finish_batch(h, fast, &viol));
-  if (viol) {  // a step of the batch needed refinement: roll back and rerun with the full graph
-    ++h->rollbacks;
-    HIPCHK(hipMemcpyAsync(h->params, h->snap, nb, hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemcpyAsync(h->m, h->snap + np, nb, hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemcpyAsync(h->v, h->snap + 2 * np, nb, hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemcpyAsync(h->count, h->snap_count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
-    TRY(check_launch(launch_sync_u(h->params, h->L, h->Up, h->s), "sync_u"));
-    TRY(capture(h, 1, true));
-    TRY(run_steps(h, n_steps, losses, false));
-    TRY(finish_batch(h, false, &viol));
+  int done = 0;
+  while (done < n_steps) {
+    const bool fast = h->fast_ok && h->fast_mode;
+    const int n = fast ? std::min(FAST_CHUNK, n_steps - done) : n_steps - done;
+    double* lo = losses ? losses + done : nullptr;
+    TRY(capture(h, 1, !fast));
+    if (fast) {  // snapshot of everything a step carries forward (Up is rebuilt from params)
+      HIPCHK(hipMemcpyAsync(h->snap, h->params, nb, hipMemcpyDeviceToDevice, h->s));
+      HIPCHK(hipMemcpyAsync(h->snap + np, h->m, nb, hipMemcpyDeviceToDevice, h->s));
+      HIPCHK(hipMemcpyAsync(h->snap + 2 * np, h->v, nb, hipMemcpyDeviceToDevice, h->s));
+      HIPCHK(hipMemcpyAsync(h->snap_count, h->count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
+      HIPCHK(hipMemsetAsync(h->viol, 0, sizeof(unsigned int), h->s));
+    }
+    TRY(run_steps(h, n, lo, fast));
+    bool viol = false;
+    TRY(finish_batch(h, fast, &viol));
+    if (viol) {  // a step of the chunk needed refinement: roll back and rerun with the full graph
+      ++h->rollbacks;
+      HIPCHK(hipMemcpyAsync(h->params, h->snap, nb, hipMemcpyDeviceToDevice, h->s));
+      HIPCHK(hipMemcpyAsync(h->m, h->snap + np, nb, hipMemcpyDeviceToDevice, h->s));
+      HIPCHK(hipMemcpyAsync(h->v, h->snap + 2 * np, nb, hipMemcpyDeviceToDevice, h->s));
+      HIPCHK(hipMemcpyAsync(h->count, h->snap_count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
+      TRY(check_launch(launch_sync_u(h->params, h->L, h->Up, h->s), "sync_u"));
+      TRY(capture(h, 1, true));
+      TRY(run_steps(h, n, lo, false));
+      TRY(finish_batch(h, false, &viol));
+    }
+    done += n;
   }
   return GPK_OK;
 }
