@@ -149,6 +149,7 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
   const int k = band * 64 + lane;
   const bool kv = k < n;
   const int cb = kv ? C.cbase[k] : 0;
+  const int nvar = kv ? C.cbase[k + 1] - cb : 0;  // distance variants of this lane's diagonal
   const int r0 = chunk * C.rb, r1 = min(n, r0 + C.rb);
   double ak[V], ad[V];
 #pragma unroll
@@ -235,14 +236,17 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
     }
     __syncthreads();
   }
-  double* pk = C.part + (size_t)chunk * C.ncls;
-  double* pd = C.part + (size_t)(C.nchunk + chunk) * C.ncls;
-  for (int e = t; e < 64 * V; e += 256) {
-    const int l = e & 63, x = e >> 6, kk = band * 64 + l;
-    if (kk < n && x < C.cbase[kk + 1] - C.cbase[kk]) {
-      pk[C.cbase[kk] + x] = red[0][x][l];
-      pd[C.cbase[kk] + x] = red[1][x][l];
-    }
+  // wave 0 writes: lane = diagonal, its class range [cb, cb + nvar) already in registers (the
+  // previous form re-read cbase per stored element: a dependent round trip per pass)
+  if (w == 0) {
+    double* pk = C.part + (size_t)chunk * C.ncls + cb;
+    double* pd = C.part + (size_t)(C.nchunk + chunk) * C.ncls + cb;
+#pragma unroll
+    for (int x = 0; x < V; ++x)
+      if (x < nvar) {
+        pk[x] = red[0][x][lane];
+        pd[x] = red[1][x][lane];
+      }
   }
   if (TR_FIRST) TR_HI(SLOT_CLASS_SUM);
   if (TR_LAST) TR_HI(SLOT_CSUM_START);
