@@ -887,9 +887,11 @@ static int read_status(gpk_handle* h) {
 
 // End of a batch (one synchronisation): non-positive-definite status, the fast graph's gate
 // violation flag, and the refinement gate of the last step, which picks the next batch's graph:
-// the fast one while max_a K00 * max diag K_a^{-1} stays 8x below REFINE_COND_LB.  The gate
-// moves slowly (a few percent per Adam step), and a step that crosses it anyway is caught by
-// the check in the fast graph's tail (viol) and rerun.
+// the fast one once max_a K00 * max diag K_a^{-1} is 8x below REFINE_COND_LB, and it stays
+// the fast one while that bound stays below REFINE_COND_LB itself (hysteresis: a fast batch
+// that crosses the gate is caught by the check in the fast graph's tail (viol) and rerun, which
+// costs one FAST_CHUNK; leaving the fast graph at the 8x margin cost ~15% on every later step
+// of C4's training, whose bound drifts into that band and stays there).
 constexpr double FAST_GRAPH_MARGIN = 8.0;
 static int finish_batch(gpk_handle* h, bool fast, bool* violated) {
   int st = 0;
@@ -909,7 +911,8 @@ static int finish_batch(gpk_handle* h, bool fast, bool* violated) {
   if (h->fast_ok) {
     double lb = 0.0;  // pst[a][1] holds max diag K^{-1} (positive, atomicMax'd as its bits)
     for (int a = 0; a < h->L.naxes; ++a) lb = std::max(lb, ps[a][0] * ps[a][1]);
-    h->fast_mode = !*violated && lb * FAST_GRAPH_MARGIN < REFINE_COND_LB;
+    const double margin = (fast && !*violated) ? 1.0 : FAST_GRAPH_MARGIN;
+    h->fast_mode = !*violated && lb * margin < REFINE_COND_LB;
   }
   return GPK_OK;
 }
