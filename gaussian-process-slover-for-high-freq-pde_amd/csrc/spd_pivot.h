@@ -8,13 +8,14 @@ namespace gpk {
 constexpr int SP = 33;  // pivot scratch stride
 typedef __attribute__((address_space(3))) double* lds_ptr;
 
+// v_rsq_f64 is 2^-24.2 relative (tools/probes/rsq_probe.hip): one Newton step leaves 4e-15,
+// two 1.4e-16.  One third-order step y (1 + e/2 + 3e^2/8), e = 1 - p y^2 (truncation ~e^3/3 =
+// 2^-70) reaches the same accuracy in 4 dependent operations after the rsq instead of 6: the
+// square roots are the serial part of the 32-column pivot chain.
 __device__ __forceinline__ double rsqrt_f64(double p) {
-  double y = __builtin_amdgcn_rsq(p);          // 2^-24.2 relative (tools/probes/rsq_probe.hip):
-                                               // one Newton step leaves 4e-15, two 1.4e-16
-  double e = fma(-p * y, y, 1.0);              // 1 - p y^2
-  y = fma(0.5 * y, e, y);
-  e = fma(-p * y, y, 1.0);
-  return fma(0.5 * y, e, y);
+  const double y = __builtin_amdgcn_rsq(p);
+  const double e = fma(-p * y, y, 1.0);
+  return fma(y * e, fma(0.375, e, 0.5), y);
 }
 
 // One workgroup (256 threads): Cholesky of the 32x32 SPD block A = L L^T (LDS, stride SP,
