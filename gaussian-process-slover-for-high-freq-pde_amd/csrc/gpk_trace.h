@@ -21,6 +21,9 @@ enum TraceSlot {
   // dispatch spread (last workgroup start) and intermediate points
   SLOT_PG_START = 47, SLOT_PG_STAGED = 48, SLOT_CSUM_START = 49, SLOT_CEVAL_START = 50,
   SLOT_GATHER_START = 51, SLOT_CSUM_LOADED = 52, SLOT_CHAIN_END = 53, SLOT_CHAIN_M1 = 54,
+  // chain, last sweep, tile (T-1, T-1) of factor 0: L^{-1} flag seen, L^{-1} in LDS, products
+  // done, outputs stored + done-counter returned; 62: the same end point, last aug tile
+  SLOT_LAST_FLAG = 58, SLOT_LAST_LDS = 59, SLOT_LAST_MMA = 60, SLOT_LAST_OUT = 61, SLOT_LAST_AUG = 62,
   SLOT_GEMM = 64,  // + 4 * stage: first wg [start, end], + 1: first wg operands loaded,
                    // + 2: first wg MFMAs done, + 3: last wg [start, end]  (stages < 16)
 };

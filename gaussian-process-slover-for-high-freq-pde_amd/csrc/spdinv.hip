@@ -465,6 +465,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     }
     if (t == 0) wait_flag(piv_rdy + k);
     __syncthreads();
+    const bool trl = t == 0 && m == 0 && k == T - 1 && I == T - 1 && J == T - 1;
+    if (trl) TR_HI(SLOT_LAST_FLAG);
     const double* Li = F.piv + (size_t)k * 1024;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -474,6 +476,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
       if (needJ) sXJ[row * SB + tx] = xj[r];
     }
     __syncthreads();
+    if (trl) TR_HI(SLOT_LAST_LDS);
     const double* sVJ = (J == I) ? sXI : sXJ;
     d4 vi = {0.0, 0.0, 0.0, 0.0}, vj = {0.0, 0.0, 0.0, 0.0};
     if (needI) vi = mma_t(sL, SA, 1, sXI, SB, 1, wr, wc, lane, vi);
@@ -498,6 +501,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     // a (k, k) panel tile)
     if (k + 1 < T && I == k + 1 && J != I) publish_tile();
     if (I == J && I == k + 2) publish_diag();  // tile (k+2, k+2) after sweep k, for pivot k + 2
+    if (trl) TR_HI(SLOT_LAST_MMA);
     __syncthreads();  // LDS is refilled next sweep
   }
   if (aug && !master) {  // upper-right block: +K^{-1} B (B_u part possibly stored transposed)
@@ -532,6 +536,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   if (t == 0 && master && m == 1) TR_LO(SLOT_CHAIN_M1);
   if (t == 0) s_last = atomicAdd(done, 1u) == (unsigned)(T * TC);  // T*TC tiles + the chain
   __syncthreads();
+  if (t == 0 && m == 0 && I == T - 1 && J == T - 1 && !master) TR_HI(SLOT_LAST_OUT);
+  if (t == 0 && m == 0 && I == T - 1 && J == TC - 1 && !master) TR_HI(SLOT_LAST_AUG);
   if (s_last && t == 0) TR_HI(SLOT_CHAIN_END);
   if (s_last) {
     for (int e = t; e < T * TC + 2 * T; e += 256)
