@@ -394,6 +394,9 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
         load_inputs(F, xpre, dpre, k, p, tx, ty, wr, wc, lane);
       }
     };
+    // L^{-1}_kp is stored right after its factorisation, but its flag is raised inside the next
+    // hop (after the first product, when the stores have drained): the chain does not stall on
+    // the write-back of every pivot (the last one is signalled at once)
     auto factor = [&](int kp) {
       if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP + kp - 1);  // (inputs in: the hop ends)
       store_quad(sP, SP, wr, wc, lane, acc);
@@ -405,7 +408,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
       const double ls = pivot_chol_inv_block<4, double*, PivotPrefetch>(sP, sM, pv, t, F.status, hook);
       for (int e = t; e < 1024; e += 256) st_sc1(F.piv + (size_t)kp * 1024 + e, sM[(e >> 5) * SP + (e & 31)]);
       if (t == 0) F.ldet[kp] = ls;
-      signal_flag(piv_rdy + kp);
+      if (kp + 1 == T) signal_flag(piv_rdy + kp);
       if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP_PIVOT + kp - 1);
       if (trm && kp == 0) TR_HI(SLOT_PIVOT0);
     };
@@ -428,7 +431,9 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
       __syncthreads();
       d4 vj = {0.0, 0.0, 0.0, 0.0};
       vj = mma_t(sM, SP, 1, sXJ, SB, 1, wr, wc, lane, vj);  // V = L_k^{-1} X_{k,k+1}
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // L^{-1}_k's stores (long drained)
       __syncthreads();
+      if (t == 0) __hip_atomic_store(piv_rdy + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       store_quad(sXJ, SB, wr, wc, lane, vj);
       __syncthreads();
       d4 prod = {0.0, 0.0, 0.0, 0.0};
