@@ -193,6 +193,31 @@ struct ChainArgs {
   double* PBa; int ldpba;                  // augmented panel buffer [p][32*(tu+td)]
 };
 int spd_chain_blocks(const int* p, int nmat, bool aug);
+// chain_kernel's dispatch slot x of factor m's grid row -> its role: tile index I*TC + J, or
+// T*TC for the pivot chain.  With ~390 workgroups on 256 CUs the dispatcher's second pass over
+// the CUs doubles up the first ~130; the grid's middle (end of row 0, start of row 1) is alone
+// on its CUs.  The pivot chain sits there (last of row 0, first of row 1), and next to it the
+// 2(T-1) tiles whose sweep-k updates feed it -- panel (k, k+1) and diagonal (k+1, k+1) -- so
+// that their hand-offs reach the chain's prefetch window; the other tiles keep their order.
+__host__ __device__ inline int chain_role(int m, int x, int T, int TC) {
+  const int nt = T * TC, nc = 2 * (T - 1);
+  // critical tiles in ascending order: (0,1), (1,1), (1,2), (2,2), ...
+  auto crit = [TC](int i) { return (i & 1) ? ((i >> 1) + 1) * (TC + 1) : (i >> 1) * (TC + 1) + 1; };
+  int r;
+  if (m == 0) {
+    if (x == nt) return nt;
+    if (x >= nt - nc) return crit(x - (nt - nc));
+    r = x;
+  } else {
+    if (x == 0) return nt;
+    if (x <= nc) return crit(x - 1);
+    r = x - 1 - nc;
+  }
+  int tile = r;  // the r-th non-critical tile
+  for (int i = 0; i < nc; ++i)
+    if (crit(i) <= tile) ++tile;
+  return tile;
+}
 // prep (nullable): the step constants are published by one extra workgroup of this launch
 hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s,
                             const PrepArgs* prep = nullptr, int q = 0);

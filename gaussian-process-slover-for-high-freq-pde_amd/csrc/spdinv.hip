@@ -274,11 +274,9 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   const int T = F.T, p = F.p;
   const int TC = T + F.tu + F.td;  // tile columns: K, then the augmented B_u, D^T columns
   if ((int)blockIdx.x > T * TC) return;
-  // the pivot chain's own workgroup (below) is tile index T*TC; its dispatch slot is the last of
-  // row 0 and the FIRST of row 1: both then sit in the grid's middle (linear ids 192, 193 of 386
-  // at C4), which the dispatcher's second pass over the CUs does not reach, so neither master
-  // shares its CU with a tile workgroup (row 1's master was the grid's last workgroup and did)
-  const int tile = (m == 0) ? (int)blockIdx.x : (blockIdx.x == 0 ? T * TC : (int)blockIdx.x - 1);
+  // the pivot chain's own workgroup (below) is tile index T*TC; it and the tiles feeding it are
+  // dispatched in the grid's middle, alone on their CUs (gpk_internal.h chain_role)
+  const int tile = chain_role(m, (int)blockIdx.x, T, TC);
   const bool master = tile == T * TC;
   const int I = master ? 0 : tile / TC, J = master ? 0 : tile % TC;
   const bool aug = J >= T;
