@@ -16,6 +16,7 @@ enum TraceSlot {
   SLOT_CLASS_EVAL = 0, SLOT_GATHER = 1, SLOT_PIVOT0_WAIT = 2, SLOT_PIVOT0 = 3,
   SLOT_SWEEP = 4,         // + k (k < 16): whole sweep launch k
   SLOT_SWEEP_PIVOT = 20,  // + k: the next-pivot factorisation inside sweep k
+  SLOT_PREFETCH_MISS = 36,  // chain, factor 0: first / last pivot whose inputs missed the prefetch
   SLOT_CLASS_SUM = 40, SLOT_PGRAD = 41, SLOT_PG_CONTRACT = 42, SLOT_PG_GROUP = 43,
   SLOT_PG_TOP = 44, SLOT_PG_UPLANE = 45, SLOT_PG_FINAL = 46,
   // dispatch spread (last workgroup start) and intermediate points

@@ -41,10 +41,12 @@ __device__ __forceinline__ double rsqrt_f64(double p) {
 // LP: the LDS pointer type -- plain double* when inlined into a kernel (address space inferred),
 // lds_ptr (address_space(3)) when called through a non-inlined function, so that the callee
 // still issues ds_read / ds_write instead of flat memory instructions.
-// Hook (optional): hook.early() runs in every thread before the barrier that ends block step 1,
-// hook.pre() before the one that ends step 4 and hook.post() right after it -- a window to poll
+// Hook (optional): hook.early() runs in every thread before the barrier that ends block step 2,
+// hook.pre() before the one that ends step 5 and hook.post() right after it -- a window to poll
 // (without waiting) for the NEXT pivot's inputs and start their loads while this factorisation
-// still has 3 block steps to go (chain_kernel's pivot chain).
+// still has 2 block steps to go (chain_kernel's pivot chain).  The flag load needs the 3 steps
+// in between to land (a read at step 4 checked at step 6 stalled every pivot by ~1 us), and a
+// check at step 4 came too early for most inputs (C4: steps 2/5 beat 1/4 by ~1%).
 struct NoPivotHook {
   __device__ void early() {}
   __device__ void pre() {}
@@ -137,10 +139,10 @@ __device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t,
         M[row * SP + cj] = accM[r];
       }
     }
-    if (kb == 1) hook.early();
-    if (kb == 4) hook.pre();
+    if (kb == 2) hook.early();
+    if (kb == 5) hook.pre();
     __syncthreads();
-    if (kb == 4) hook.post();
+    if (kb == 5) hook.post();
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) M[(16 * wr + lk + 4 * r) * SP + cj] = accM[r];

@@ -412,6 +412,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     };
     factor(0);  // acc = tile (0, 0) of K, gathered above
     for (int k = 0; k + 1 < T; ++k) {
+      if (trm && !s_pre) { TR_LO(SLOT_PREFETCH_MISS); TR_HI(SLOT_PREFETCH_MISS); }
       if (!s_pre) {  // (uniform) not yet published at the prefetch point: wait and load now
         if (t == 0) {
           wait_flag(panel_rdy + k * TC + k + 1);
