@@ -8,21 +8,27 @@ Kronecker collocation grid, Matern52_Cos_1d (GP-HM-StM), Q = 30, fp64, jitter 1e
 HBM before the timed region starts.  Synthetic data: the reference's grid/source/boundary
 construction with U ~ 0.1 N(0,1) (seed = rank).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
-solving an independent 256^2 problem (replicas, weak scaling, no data-path collective; see
-DESIGN.md §Multi-GPU).  Timing: barrier + device sync on both sides of exactly --steps steps,
-max over ranks; value = total steps of all ranks / that time.
+Multi-GPU: `bench.py --gpus N` starts N ranks of itself (one process per GPU, the
+torch.distributed.run environment: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*) before anything
+touches a GPU, or runs as one of the ranks when launched by torch.distributed.run (then --gpus
+must equal WORLD_SIZE).  Each rank solves an independent 256^2 problem (replicas, weak scaling,
+no data-path collective).  Timing: barrier + device sync on both sides of exactly
+--steps steps, max over ranks; value = total steps of all ranks / that time.  With N > 1 the
+line also carries `sharded`: ONE C4 and ONE C5 problem row-sharded over the N ranks with RCCL
+(strong scaling of a single problem).
 
 Also reported: the dominant kernel's roofline (HIP events on the library's stream, algorithmic
-bytes/flops per launch), fp64 SPD factor+inverse GFLOP/s, the CPU
-oracle timed on this host on a bounded sample (rank 0, N = 1 only), and `large_factors`: the
-MFMA-bound kernels at C5's 4096^2 size (GEMM TF/s and fraction of the fp64 peak, the large SPD
-inverse, C5 ms/step; rank 0, N = 1 only, --no-large to skip).
+bytes/flops per launch), fp64 SPD factor+inverse GFLOP/s, a step(1)-per-call
+rate (the reference's loop shape), the CPU oracle timed on this host on bounded samples (all
+cores and 1 core; rank 0, N = 1 only; child processes, so no thread setting leaks into the GPU
+process), and `large_factors`: the MFMA-bound kernels at C5's 4096^2 size (rank 0, N = 1).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -34,7 +40,6 @@ METRIC = "log-joint iters/sec + fp64 Cholesky GFLOP/s, 2D Poisson 256^2, 1-8 GPU
 # launches per step of the fast step graph (sweep: T = p/32 in the per-sweep inverse; the
 # persistent chain inverse is one launch; 3 GEMM stages with the augmented chain, else 5)
 KERNEL_LAUNCHES = {"spd_chain": 1, "sweep": None, "gemm_B": 3, "pgrad": 1, "assemble": 1}
-
 
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench (tools/gpu_round.sh), summarised by
 # tools/pmc_summary.py: HBM-side bytes per launch (2*FETCH + WRITE, MI355X_MICROARCH.md §HBM)
@@ -54,20 +59,21 @@ def pmc_traffic(kernel):
         return None
 
 
-def cpu_baseline(config, seconds, max_steps=400):
+# ------------------------------------------------------------------------------------------
+# CPU baseline (test infrastructure: the oracle, never the product)
+# ------------------------------------------------------------------------------------------
+def cpu_baseline(config, seconds, threads, max_steps=400):
     """The CPU oracle (oracle/gp_oracle.py: NumPy/SciPy LU + OpenMP C fields) on the same
-    workload, bounded sample of `seconds` of work (test infrastructure; never the product)."""
+    workload, a bounded sample of `seconds` of work.  Runs in a child process of rank 0
+    (`--cpu-baseline-only`): OMP / BLAS thread counts are fixed before NumPy loads."""
     import numpy as np
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    os.environ["OMP_NUM_THREADS"] = str(threads)
-    os.environ.setdefault("OMP_WAIT_POLICY", "PASSIVE")
     try:
         # OpenMP (C fields) gets the cores; BLAS runs single-threaded: a multithreaded
         # OpenBLAS contending with the OpenMP pool made a 256^2 step 6x slower (measured)
         from threadpoolctl import threadpool_limits
-        limiter = threadpool_limits(limits=1, user_api="blas")
+        threadpool_limits(limits=1, user_api="blas")
     except Exception:  # pragma: no cover
-        limiter = None
+        pass
     from oracle import gp_oracle as O
     from gpk.problems import CONFIGS
     cfg = CONFIGS[config]
@@ -85,22 +91,35 @@ def cpu_baseline(config, seconds, max_steps=400):
         params, st = opt.update(g, st, params)
         steps += 1
     dt = time.perf_counter() - t0
-    if limiter is not None:
-        limiter.unregister() if hasattr(limiter, "unregister") else None
     return {"value": steps / dt, "unit": "iters/s", "cores": threads, "kind": "port",
             "sample": f"{steps} full steps (loss+grad+Adam) of {config} {cfg['n']}x{cfg['n']}, "
                       f"{dt:.1f} s, oracle/gp_oracle.py (SciPy LU, 1 BLAS thread + OpenMP/libmvec "
-                      f"C fields on {threads} threads)"}
+                      f"C fields on {threads} thread(s))"}
 
 
+def cpu_baseline_child(config, seconds, threads):
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_WAIT_POLICY="PASSIVE",
+               OPENBLAS_NUM_THREADS="1", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--config", config,
+           "--cpu-seconds", str(seconds), "--cpu-threads", str(threads)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=10 * seconds + 300)
+    if r.returncode != 0:
+        return {"value": None, "error": r.stderr.strip().splitlines()[-1:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+# ------------------------------------------------------------------------------------------
+# GPU sections
+# ------------------------------------------------------------------------------------------
 def large_factors(steps=3):
     """The MFMA-bound end of the path on C5's 4096^2 grid (BASELINE.json configs[4]): the
     128x128-tile GEMM stage gemm_B (S = A K2^{-1} and the residual R = beta D1 A + Bt D2^T - F:
-    three 4096^3 products), the 64-wide SPD inverse of both 4096 factors (n^3 flops each =
+    three 4096^3 products), the SPD factor + inverse of both 4096 factors (n^3 flops each =
     potrf + potri) and whole steps.  Not the headline; shows fp64 MFMA utilisation at size."""
     from gpk.problems import make_solver
     s = make_solver("C5", seed=0)
     try:
+        s.prepare(steps)
         s.step(1)
         t0 = time.perf_counter()
         s.step(steps)
@@ -109,97 +128,51 @@ def large_factors(steps=3):
         inv_us = s.time_spd_inverse(3)
         n = 4096
         tus, tfl, _ = s.bench_kernel("spd_tiles", 3)
+        path = s.inverse_path()
     finally:
         s.close()
     gemm_tf = fl / (us * 1e-6) / 1e12
     return {"config": "C5: advection 4096x4096, Matern52_Cos_1d, Q=30, fp64", "step_ms": step_ms,
-            "gemm_B_us": us, "gemm_tflops": gemm_tf, "gemm_mfma_frac": gemm_tf / PEAK_F64_TFLOPS,
-            "spd_inverse_ms": inv_us / 1e3, "cholesky_gflops": 2 * n ** 3 / (inv_us * 1e-6) / 1e9,
+            "inverse_path": path, "gemm_B_us": us, "gemm_tflops": gemm_tf,
+            "gemm_mfma_frac": gemm_tf / PEAK_F64_TFLOPS, "spd_inverse_ms": inv_us / 1e3,
+            "cholesky_gflops": 2 * n ** 3 / (inv_us * 1e-6) / 1e9,
             "spd_update_tflops": tfl / (tus * 1e-6) / 1e12}
 
 
-def main_sharded(a):
-    """One 2D problem (--config) row-sharded over all ranks (gpk/shard.py): every rank runs its
-    rows of every product, RCCL all-gathers / all-reduces inside the step graph.  value = steps
-    of the single problem per second (strong scaling)."""
+def sharded_section(a, ctx, configs=("C4", "C5")):
+    """ONE problem per config row-sharded over all ranks (gpk/shard.py: rows of every product
+    per rank, RCCL all-gathers / all-reduces inside the step graph).  value = steps/s of the
+    single problem (strong scaling)."""
     from gpk import replicas, shard
-    from gpk.problems import CONFIGS
-    ctx = replicas.init("nccl")
-    cfg = CONFIGS[a.config]
-    s = shard.make_sharded_solver(a.config, ctx, seed=0)
-    s.step(a.warmup)
-    replicas.barrier(ctx)
-    t0 = time.perf_counter()
-    losses = s.step(a.steps)
-    t1 = time.perf_counter()
-    replicas.barrier(ctx)
-    dt = replicas.max_over_ranks(t1 - t0, ctx)
-    if ctx.rank == 0:
-        n = cfg["n"]
-        print(json.dumps({
-            "metric": METRIC, "value": a.steps / dt, "unit": "iters/s", "n_gpus": ctx.world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: reference grid/source/boundary, U ~ 0.1 N(0,1) (seed 0, same on every rank)",
-            "config": {"workload": f"{a.config}: one {n}x{n} 2D problem row-sharded over {ctx.world} GPU(s)",
-                       "grid": [n, n], "Q": 30, "kernel": cfg["kernel"], "equation": cfg["equation"],
-                       "parallelism": f"row-sharded x{ctx.world} (RCCL all-gather / all-reduce)"},
-            "roofline": None, "cpu_baseline": None, "final_loss": float(losses[-1])}), flush=True)
-    s.close()
-    replicas.shutdown(ctx)
+    out = {}
+    for cid in configs:
+        steps = a.sharded_steps if cid == "C4" else max(2, a.sharded_steps // 10)
+        s = shard.make_sharded_solver(cid, ctx, seed=0)
+        try:
+            s.prepare(steps)
+            s.step(2)
+            replicas.barrier(ctx)
+            t0 = time.perf_counter()
+            s.step(steps)
+            t1 = time.perf_counter()
+            replicas.barrier(ctx)
+        finally:
+            s.close()
+        dt = replicas.max_over_ranks(t1 - t0, ctx)
+        out[cid] = {"value": steps / dt, "unit": "iters/s", "ms_per_step": dt / steps * 1e3,
+                    "steps": steps, "ranks": ctx.world}
+    return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="C4")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel-iters", type=int, default=50)
-    ap.add_argument("--no-large", action="store_true", help="skip the C5-size MFMA section")
-    ap.add_argument("--mode", choices=["replicas", "sharded"], default="replicas",
-                    help="replicas: one independent problem per GPU (weak scaling, the default); "
-                         "sharded: ONE 2D problem row-sharded over the GPUs with RCCL (strong scaling)")
-    a = ap.parse_args()
-    if a.mode == "sharded":
-        return main_sharded(a)
-
-    from gpk import replicas
-    from gpk.problems import CONFIGS, make_solver
-    ctx = replicas.init("nccl")
-    world, rank, local = ctx.world, ctx.rank, ctx.local
-    cfg = CONFIGS[a.config]
-    s = make_solver(a.config, seed=rank, device=local)
-    s.step(a.warmup)                     # warm-up: graph capture + caches
-    replicas.barrier(ctx)
-    t0 = time.perf_counter()
-    fast_graph, rb0 = s.graph_mode()     # graph the timed batch starts on (refinement gate closed?)
-    losses = s.step(a.steps)             # exactly K steps; returns after a device sync
-    t1 = time.perf_counter()
-    replicas.barrier(ctx)
-    fast_end, rb1 = s.graph_mode()       # graph it ends on; chunks rerun inside the timed batch
-    rollbacks = rb1 - rb0
-    dt = replicas.max_over_ranks(t1 - t0, ctx)
-    value = world * a.steps / dt
-
-    # fp64 SPD factor+inverse rate: potrf + potri = n^3 flops per Kronecker factor
-    inv_us = s.time_spd_inverse(20)
+def kernel_roofline(s, cfg, iters):
+    """Per-kernel device timings (HIP events on the library's stream); the dominant kernel =
+    largest device time per step, priced against its roofline."""
     n = cfg["n"]
-    nfac = 2 if cfg["dim"] == 2 else 1
-    chol_gflops = nfac * n ** 3 / (inv_us * 1e-6) / 1e9
-
-    # per-kernel timings; the dominant kernel = largest device time per step
     T = (n + 31) // 32
     kern = {}
-    try:  # the step's SPD inverse: the persistent chain launch when the factors are small
-        s.bench_kernel("spd_chain", 1)
-        spd = "spd_chain"
-    except Exception:
-        spd = "sweep"
+    spd = "spd_chain" if s.inverse_path() in ("chain", "chain_aug") else "sweep"
     for name in ([spd, "gemm_B", "pgrad", "assemble"] if cfg["dim"] == 2 else [spd, "assemble"]):
-        us, fl, by = s.bench_kernel(name, a.kernel_iters)
+        us, fl, by = s.bench_kernel(name, iters)
         launches = T if name == "sweep" else KERNEL_LAUNCHES[name]
         kern[name] = dict(us=us, flops=fl, bytes=by, per_step_us=us * launches)
     dom = max(kern, key=lambda k: kern[k]["per_step_us"])
@@ -217,55 +190,198 @@ def main():
     roof["avg_launch_us"] = d["us"]
     roof["alg_flops_per_launch"] = d["flops"]
     roof["alg_bytes_per_launch"] = d["bytes"]
+    # K-assembly HBM rate the north star asks for: K and D written per launch (16 n^2 B per
+    # axis) over the assembly launch's time (class values + gather when the chain gathers)
+    asm = kern.get("assemble")
+    return roof, {k: round(v["us"], 3) for k, v in kern.items()}, asm
 
-    large = None
-    if rank == 0 and world == 1 and not a.no_large:
+
+class _DryRunSolver:
+    """--dry-run: a stand-in with the solver's stepping interface and no GPU (tests of the
+    launcher / rank plumbing on CPU).  Its numbers are not measurements."""
+
+    def __init__(self, seed):
+        self.seed = seed
+
+    def prepare(self, n):
+        pass
+
+    def step(self, n):
+        time.sleep(1e-4 * n)
+        return [float(self.seed)] * n
+
+    def graph_mode(self):
+        return False, 0
+
+    def inverse_path(self):
+        return "dry-run"
+
+    def close(self):
+        pass
+
+
+def spawn_ranks(n):
+    """One process per GPU, started before this process touches a GPU (children get the
+    torch.distributed.run environment); exits with the worst child status."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    sys.exit(bad[0] if bad else 0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="C4")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-iters", type=int, default=50)
+    ap.add_argument("--step1-calls", type=int, default=200)
+    ap.add_argument("--no-large", action="store_true", help="skip the C5-size MFMA section")
+    ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the row-sharded section")
+    ap.add_argument("--sharded-steps", type=int, default=50)
+    ap.add_argument("--sharded-timeout", type=float, default=240.0)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/rank plumbing only: gloo, stand-in solver, no GPU (tests)")
+    a = ap.parse_args()
+    if a.cpu_baseline_only:
+        print(json.dumps(cpu_baseline(a.config, a.cpu_seconds, a.cpu_threads)), flush=True)
+        return
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        return spawn_ranks(a.gpus)
+    if env_world is not None and int(env_world) != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_world}")
+
+    from gpk import replicas
+    from gpk.problems import CONFIGS, make_solver
+    ctx = replicas.init("gloo" if a.dry_run else "nccl")
+    world, rank, local = ctx.world, ctx.rank, ctx.local
+    cfg = CONFIGS[a.config]
+    s = _DryRunSolver(rank) if a.dry_run else make_solver(a.config, seed=rank, device=local)
+    s.prepare(a.steps)                   # every graph the timed call can launch, built untimed
+    s.step(a.warmup)                     # warm-up steps
+    replicas.barrier(ctx)
+    t0 = time.perf_counter()
+    fast_graph, rb0 = s.graph_mode()     # graph the timed batch starts on (refinement gate closed?)
+    losses = s.step(a.steps)             # exactly K steps; returns after a device sync
+    t1 = time.perf_counter()
+    replicas.barrier(ctx)
+    fast_end, rb1 = s.graph_mode()       # graph it ends on; chunks rerun inside the timed batch
+    rollbacks = rb1 - rb0
+    dt = replicas.max_over_ranks(t1 - t0, ctx)
+    value = world * a.steps / dt
+
+    extra = {}
+    if not a.dry_run:
+        # the reference's loop shape: one step() call per iteration (model_GP_solver_2d.py:285-300)
+        s.step(5)
+        t = time.perf_counter()
+        for _ in range(a.step1_calls):
+            s.step(1)
+        extra["step1_per_call"] = {"value": a.step1_calls / (time.perf_counter() - t), "unit": "iters/s",
+                                   "calls": a.step1_calls}
+        # fp64 SPD factor+inverse rate: potrf + potri = n^3 flops per Kronecker factor
+        inv_us = s.time_spd_inverse(20)
+        n = cfg["n"]
+        nfac = 2 if cfg["dim"] == 2 else 1
+        extra["cholesky_gflops"] = nfac * n ** 3 / (inv_us * 1e-6) / 1e9
+        extra["spd_inverse_us"] = inv_us
+        roof, kus, asm = kernel_roofline(s, cfg, a.kernel_iters)
+        extra["roofline"] = roof
+        extra["kernels_us"] = kus
+        extra["assembly_hbm_gbs"] = asm["bytes"] / (asm["us"] * 1e-6) / 1e9 if asm else None
+    final_loss = float(losses[-1])
+    path = s.inverse_path()
+    s.close()
+
+    if world > 1 and not a.dry_run and not a.no_sharded:
+        # strong scaling of ONE problem; a watchdog keeps a stuck collective from eating the line
+        done = threading.Event()
+        result = {}
+
+        def watchdog():
+            if not done.wait(a.sharded_timeout):
+                result["sharded"] = {"error": f"timeout after {a.sharded_timeout:.0f} s"}
+                if rank == 0:
+                    emit(a, value, dt, world, fast_graph, fast_end, rollbacks, final_loss, path, extra, result)
+                os._exit(0)
+        threading.Thread(target=watchdog, daemon=True).start()
         try:
-            large = large_factors()
+            result["sharded"] = sharded_section(a, ctx)
         except Exception as e:  # reported, never required
-            large = {"error": f"{type(e).__name__}: {e}"}
+            result["sharded"] = {"error": f"{type(e).__name__}: {e}"}
+        done.set()
+        extra.update(result)
 
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        try:
-            cpu = cpu_baseline(a.config, a.cpu_seconds)
-        except Exception as e:  # the baseline is reported, never required
-            cpu = {"value": None, "error": f"{type(e).__name__}: {e}"}
+    if rank == 0 and world == 1 and not a.dry_run:
+        if not a.no_large:
+            try:
+                extra["large_factors"] = large_factors()
+            except Exception as e:  # reported, never required
+                extra["large_factors"] = {"error": f"{type(e).__name__}: {e}"}
+        if not a.no_cpu_baseline:
+            extra["cpu_baseline"] = cpu_baseline_child(a.config, a.cpu_seconds, a.cpu_threads)
+            extra["cpu_baseline_1core"] = cpu_baseline_child(a.config, a.cpu_seconds, 1)
 
     if rank == 0:
-        out = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "iters/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": dt / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic: reference grid/source/boundary of poisson_2d-sin_sin, U ~ 0.1 N(0,1) seeded per rank",
-            "config": {"workload": f"{a.config}: 2D Poisson 256x256 Kronecker grid, Matern52_Cos_1d, Q=30, fp64"
-                       if a.config == "C4" else a.config,
-                       "grid": [n, n] if cfg["dim"] == 2 else [n], "Q": 30, "kernel": cfg["kernel"],
-                       "equation": cfg["equation"],
-                       "parallelism": f"replicas x{world} (one independent problem per GPU)"},
-            "cholesky_gflops": chol_gflops,
-            "spd_inverse_us": inv_us,
-            "roofline": roof,
-            "kernels_us": {k: round(v["us"], 3) for k, v in kern.items()},
-            "cpu_baseline": cpu,
-            "large_factors": large,
-            "final_loss": float(losses[-1]),
-            # step graph of the timed batch: "fast" = refinement GEMM stages left out (gate closed,
-            # checked every step; a step needing refinement reruns its 64-step chunk on the full
-            # graph, counted in rollbacks); "fast_at_end" = the graph the last chunk ran
-            "step_graph": {"fast": bool(fast_graph), "fast_at_end": bool(fast_end), "rollbacks": int(rollbacks)},
-        }
-        print(json.dumps(out), flush=True)
-    s.close()
+        emit(a, value, dt, world, fast_graph, fast_end, rollbacks, final_loss, path, extra)
     replicas.shutdown(ctx)
+
+
+def emit(a, value, dt, world, fast_graph, fast_end, rollbacks, final_loss, path, extra, more=None):
+    from gpk.problems import CONFIGS
+    cfg = CONFIGS[a.config]
+    n = cfg["n"]
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "iters/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": ("dry-run stand-in solver, NOT a measurement" if a.dry_run else
+                 "synthetic: reference grid/source/boundary of poisson_2d-sin_sin, U ~ 0.1 N(0,1) seeded per rank"),
+        "config": {"workload": f"{a.config}: 2D Poisson 256x256 Kronecker grid, Matern52_Cos_1d, Q=30, fp64"
+                   if a.config == "C4" else a.config,
+                   "grid": [n, n] if cfg["dim"] == 2 else [n], "Q": 30, "kernel": cfg["kernel"],
+                   "equation": cfg["equation"],
+                   "parallelism": f"replicas x{world} (one independent problem per GPU)"},
+        "inverse_path": path,
+        "cholesky_gflops": extra.get("cholesky_gflops"),
+        "spd_inverse_us": extra.get("spd_inverse_us"),
+        "roofline": extra.get("roofline"),
+        "kernels_us": extra.get("kernels_us"),
+        "assembly_hbm_gbs": extra.get("assembly_hbm_gbs"),
+        "step1_per_call": extra.get("step1_per_call"),
+        "cpu_baseline": extra.get("cpu_baseline"),
+        "cpu_baseline_1core": extra.get("cpu_baseline_1core"),
+        "large_factors": extra.get("large_factors"),
+        "sharded": (more or extra).get("sharded"),
+        "final_loss": final_loss,
+        # step graph of the timed batch: "fast" = refinement GEMM stages left out (gate closed,
+        # checked every step; a step needing refinement reruns its 64-step chunk on the full
+        # graph, counted in rollbacks); "fast_at_end" = the graph the last chunk ran
+        "step_graph": {"fast": bool(fast_graph), "fast_at_end": bool(fast_end), "rollbacks": int(rollbacks)},
+    }
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

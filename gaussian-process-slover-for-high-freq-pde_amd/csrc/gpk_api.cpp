@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -32,6 +33,7 @@
 using namespace gpk;
 
 static thread_local std::string g_err;
+static std::atomic<int> g_chain_cap{0};  // gpk_set_chain_capacity override (0: query the device)
 static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -122,7 +124,7 @@ struct gpk_handle {
   bool bigspd = false;                // large-factor SPD inverse (spdinv_big.hip)
   bool chain = false;                 // small factors: persistent one-launch inverse (chain_kernel)
   bool chain_aug = false;             // ... which also solves A, Bt^T and K^{-1} D^T (2D, unsharded)
-  unsigned int* cflags[2] = {};       // its hand-off flags [T*(T+taug) + T + 1] per factor
+  unsigned int* cflags[2] = {};       // its hand-off flags [T*(T+taug) + 2T + 1] per factor
   double *PD[2] = {}, *PBa[2] = {};   // K_a^{-1} D_a^T; augmented panel buffers
   ClassArgs cls[2] = {};              // distance classes per axis (ncls = 0: per-pair path)
   double* rvec = nullptr;            // 1D refinement residual
@@ -1044,7 +1046,7 @@ static std::vector<double> init_params(const gpk_problem* p, const Layout& L, do
 }
 
 static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nranks, bool shard,
-                       gpk_handle** out) {
+                       gpk_handle** out, bool local_group = false) {
   if (!p || !out) return fail(GPK_EINVAL, "NULL argument");
   *out = nullptr;
   if (p->dim != 1 && p->dim != 2) return fail(GPK_EINVAL, "dim must be 1 or 2");
@@ -1078,11 +1080,31 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     const int pmax = std::max(L.p1, L.dim == 2 ? L.p2 : 0);
     h->bigspd = (p->flags & GPK_FLAG_FORCE_BIG_SPD) != 0 ||
                 (!(p->flags & GPK_FLAG_FORCE_SMALL_SPD) && pmax >= SPD_BIG_MIN);
+    // The persistent chain inverse needs its whole grid co-resident: the grid (workgroups of
+    // every factor's row, the widest row times the factors) must fit the device's capacity for
+    // the chain variant the step launches (occupancy per CU x CUs, so a CU-partitioned device
+    // falls back to the per-sweep launches), and handles of an in-process rank group -- which
+    // launch concurrently on one device from several host threads -- never use it.
     const int pp[2] = {L.p1, L.p2};
-    h->chain = !h->bigspd && !(p->flags & GPK_FLAG_NO_CHAIN) &&
-               spd_chain_blocks(pp, L.naxes, false) <= CHAIN_MAX_BLOCKS;
+    const int deriv = p->eq == GPK_ADVECTION ? 1 : 2;
+    int cap = g_chain_cap.load();
+    if (cap <= 0) {
+      DevSwitch dsw(p->device);
+      const bool gather = !(p->flags & GPK_FLAG_NO_DCLASS);  // (gather mode needs classes; the
+      cap = std::min(spd_chain_capacity(deriv, gather),       //  per-pair mode's footprint is
+                     spd_chain_capacity(deriv, false));        //  bounded by the same check)
+    }
+    cap = std::min(cap, CHAIN_MAX_BLOCKS);
+    auto grid_blocks = [&](bool aug) {  // launch_spd_chain's grid: (max_a T_a TC_a + 1) x factors
+      const int cols = (L.p1 + (L.naxes == 2 ? L.p2 : 0)) / 32;
+      int wide = 0;
+      for (int a = 0; a < L.naxes; ++a) wide = std::max(wide, (pp[a] / 32) * (pp[a] / 32 + (aug ? cols : 0)) + 1);
+      return wide * L.naxes;
+    };
+    const bool in_group = shard && local_group && nranks > 1;
+    h->chain = !h->bigspd && !in_group && !(p->flags & GPK_FLAG_NO_CHAIN) && grid_blocks(false) <= cap;
     h->chain_aug = h->chain && L.dim == 2 && !shard && !(p->flags & GPK_FLAG_NO_CHAIN_AUG) &&
-                   spd_chain_blocks(pp, L.naxes, true) <= CHAIN_MAX_BLOCKS;
+                   grid_blocks(true) <= cap;
   }
   auto bail = [&](int rc) {
     gpk_destroy(h);
@@ -1267,7 +1289,7 @@ int gpk_group_create(const gpk_problem* p, double freq_scale, int32_t nranks, gp
   g->slot.assign(nranks, nullptr);
   for (int r = 0; r < nranks; ++r) out[r] = nullptr;
   for (int r = 0; r < nranks; ++r) {
-    int rc = create_impl(p, freq_scale, r, nranks, true, &out[r]);
+    int rc = create_impl(p, freq_scale, r, nranks, true, &out[r], true);
     if (rc != GPK_OK) {
       for (int k = 0; k < r; ++k) gpk_destroy(out[k]);
       return rc;
@@ -1509,6 +1531,20 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
   return GPK_OK;
 }
 
+int gpk_prepare(gpk_handle* h, int32_t n_steps) {
+  if (!h) return fail(GPK_EINVAL, "NULL handle");
+  if (n_steps < 0) return fail(GPK_EINVAL, "n_steps < 0");
+  if (h->shard && !h->comm->capturable()) return GPK_OK;  // in-process groups run eagerly
+  DevSwitch ds(h->dev);
+  for (int refine = 0; refine < 2; ++refine) {
+    if (!refine && !h->fast_ok) continue;
+    TRY(capture(h, 1, refine != 0));
+    if (!h->shard && n_steps >= STEP_GRAPH_REPS) TRY(capture(h, 1, refine != 0, STEP_GRAPH_REPS));
+  }
+  HIPCHK(hipStreamSynchronize(h->s));
+  return GPK_OK;
+}
+
 int gpk_trace_reset(void) {
   trace_reset_assemble();
   trace_reset_spdinv();
@@ -1549,6 +1585,17 @@ int gpk_distance_classes(const double* x, int32_t n, int32_t* ncls, int32_t* vma
 int gpk_class_count(const gpk_handle* h, int32_t axis, int32_t* ncls) {
   if (!h || !ncls || axis < 0 || axis >= h->L.naxes) return fail(GPK_EINVAL, "bad argument");
   *ncls = h->cls[axis].ncls;
+  return GPK_OK;
+}
+
+int gpk_set_chain_capacity(int32_t workgroups) {
+  g_chain_cap.store(workgroups > 0 ? workgroups : 0);
+  return GPK_OK;
+}
+
+int gpk_inverse_path(const gpk_handle* h, int32_t* path) {
+  if (!h || !path) return fail(GPK_EINVAL, "NULL argument");
+  *path = h->bigspd ? GPK_INV_BIG : h->chain_aug ? GPK_INV_CHAIN_AUG : h->chain ? GPK_INV_CHAIN : GPK_INV_SWEEP;
   return GPK_OK;
 }
 

@@ -177,8 +177,9 @@ hipError_t launch_spd_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
 // sweeps (the sweep operator's upper-right block), which end as K^{-1} B_u and K^{-1} D^T --
 // the step's first solves (A = K1^{-1} U, Bt^T = K2^{-1} U^T) and the derivative solves
 // (K^{-1} D^T) without GEMM launches of their own.
-// Every workgroup waits on others, so the grid must be co-resident: at most two per CU
-// (235 VGPRs, 50 KB LDS each fit twice).
+// Every workgroup waits on others, so the grid must be co-resident: gpk_create checks the
+// grid against spd_chain_capacity (occupancy per CU x CUs: two per CU on a full MI355X -- 235
+// VGPRs, 50 KB LDS each fit twice -- i.e. 512) and caps it at CHAIN_MAX_BLOCKS.
 constexpr int CHAIN_MAX_BLOCKS = 512;
 struct ChainArgs {
   double* X; double* PB; double* piv; double* ldet; double* pst; int* status;
@@ -193,6 +194,8 @@ struct ChainArgs {
   double* PBa; int ldpba;                  // augmented panel buffer [p][32*(tu+td)]
 };
 int spd_chain_blocks(const int* p, int nmat, bool aug);
+// co-resident workgroups of the chain kernel variant on the current device (0 if unknown)
+int spd_chain_capacity(int deriv, bool gather);
 // chain_kernel's dispatch slot x of factor m's grid row -> its role: tile index I*TC + J, or
 // T*TC for the pivot chain.  With ~390 workgroups on 256 CUs the dispatcher's second pass over
 // the CUs doubles up the first ~130; the grid's middle (end of row 0, start of row 1) is alone

@@ -35,7 +35,7 @@ __device__ __forceinline__ double rsqrt_f64(double p) {
 // B become M_B = X.  Only entries that change are published to LDS, and the entries read in a
 // block step (A's column block B and diagonal block, M's rows B) never change in it, so one
 // barrier per block suffices and M needs no second buffer.  The 4x4 square roots use
-// v_rsq_f64 + two Newton steps.  Results are bitwise those of the VALU form it replaced (MFMA
+// v_rsq_f64 + one third-order correction (rsqrt_f64 above).  Results are bitwise those of the VALU form it replaced (MFMA
 // f64 accumulates the 4 products in the same order); 5.2 us vs 6.6 us per factorisation
 // (tools/probes/pivot_mfma_probe.hip).
 // LP: the LDS pointer type -- plain double* when inlined into a kernel (address space inferred),

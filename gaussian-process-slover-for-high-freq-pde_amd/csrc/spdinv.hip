@@ -205,7 +205,8 @@ __global__ __launch_bounds__(256) void sweep_kernel(SpdBatch b, int k) {
 //     sc1 load, a barrier, then sc1 loads of the payload.
 // The per-sweep critical path is the pivot owner's hop (poll + loads + two MFMA passes) plus its
 // factorisation.  All workgroups wait on one another, so the grid must be co-resident: used
-// when sum_m T_m^2 <= CHAIN_MAX_BLOCKS (one workgroup per CU at most).  The arithmetic is the
+// only when the grid fits the device's co-resident capacity (spd_chain_capacity: occupancy per CU
+// x CUs; two per CU on a full MI355X) and at most CHAIN_MAX_BLOCKS.  The arithmetic is the
 // sweep kernel's operation for operation: the results are bitwise equal.
 struct ChainFactor {
   double* X;            // in: assembled K (read mode); out: K^{-1}
@@ -410,6 +411,14 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
       if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP_PIVOT + kp - 1);
       if (trm && kp == 0) TR_HI(SLOT_PIVOT0);
     };
+    // refinement gate: K_00 = max diag K (stationary kernel + jitter), and max diag K^{-1}
+    // zeroed here -- before piv_rdy[0] is raised (the vmcnt(0) ahead of that flag drains these
+    // stores), so it precedes every diagonal tile's atomicMax, which waits on all piv_rdy[k]
+    if (t == 0) {
+      st_sc1(F.pst, acc[0]);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(F.pst + 1), 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
     factor(0);  // acc = tile (0, 0) of K, gathered above
     for (int k = 0; k + 1 < T; ++k) {
       if (trm && !s_pre) { TR_LO(SLOT_PREFETCH_MISS); TR_HI(SLOT_PREFETCH_MISS); }
@@ -442,11 +451,6 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     }
   } else {
     if (trm && tile == 0) TR_LO(SLOT_GATHER);
-    if (I == 0 && J == 0 && t == 0) {
-      F.pst[0] = acc[0];  // K_00 = max diag K (stationary kernel + jitter): refinement gate
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(F.pst + 1), 0ull, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);  // max diag K^{-1}, atomicMax'd at the end
-    }
     if (I == 0 && J != 0) publish_tile();  // row 0 is the panel of sweep 0
     if (I == 1 && J == 1 && T > 1) publish_diag();  // tile (1, 1) as it is before sweep 0
   }
@@ -548,6 +552,22 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
       __hip_atomic_store(F.flags + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// Workgroups of chain_kernel<DERIV, GATHER> the current device keeps resident at once:
+// occupancy per CU (its VGPR / LDS footprint) x the CUs this device (or partition) exposes.
+int spd_chain_capacity(int deriv, bool gather) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  hipError_t e;
+  if (!gather)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, chain_kernel<0, false>, 256, 0);
+  else if (deriv == 1)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, chain_kernel<1, true>, 256, 0);
+  else
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, chain_kernel<2, true>, 256, 0);
+  return e == hipSuccess ? per * cus : 0;
 }
 
 int spd_chain_blocks(const int* p, int nmat, bool aug) {

@@ -133,6 +133,12 @@ class DeviceSolver:
         check(_lib.load().gpk_graph_mode(self._h, ctypes.byref(f), ctypes.byref(r)))
         return bool(f.value), int(r.value)
 
+    def inverse_path(self):
+        """The SPD inverse the step uses: 'sweep' | 'chain' | 'chain_aug' | 'big'."""
+        v = ctypes.c_int32()
+        check(_lib.load().gpk_inverse_path(self._h, ctypes.byref(v)))
+        return _lib.INV_PATH_NAMES[int(v.value)]
+
     # -- lifecycle ---------------------------------------------------------------------
     def class_counts(self):
         """Distance classes the step evaluates per axis (0: per-pair kernels)."""
@@ -192,6 +198,10 @@ class DeviceSolver:
         out = np.empty(max(int(n), 1))
         check(_lib.load().gpk_step(self._h, int(n), dptr(out) if losses else None))
         return out[:n] if losses else None
+
+    def prepare(self, n=1):
+        """Build every step graph a step(n) call can launch, without stepping (gpk_prepare)."""
+        check(_lib.load().gpk_prepare(self._h, int(n)))
 
     def predict(self, xte1, xte2=None):
         x1 = f64(xte1).reshape(-1)
@@ -273,6 +283,12 @@ def kernel_matrices(kind, x1, x2, paras, jitter=0.0, deriv=0):
                                   dptr(ll), dptr(fr), lw.size, float(jitter), dptr(K),
                                   dptr(D) if deriv else None))
     return K, D
+
+
+def set_chain_capacity(workgroups):
+    """Override the co-resident workgroup budget gpk_create checks the persistent chain inverse
+    against (0: query the device).  Tests use it to force the per-sweep fallback."""
+    check(_lib.load().gpk_set_chain_capacity(int(workgroups)))
 
 
 def comm_unique_id():

@@ -134,6 +134,17 @@ int gpk_kernel_pairs(int32_t kind, int32_t deriv, const double* x1, const double
 int gpk_create(const gpk_problem* prob, double freq_scale, gpk_handle** out);
 int gpk_destroy(gpk_handle* h);
 
+/* SPD inverse path a handle's step uses (chosen at gpk_create from the factor sizes, the flags
+ * and the device): 32-wide per-sweep launches, the persistent chain (K^{-1} only / augmented
+ * with the first solves), or the large-factor path. */
+enum { GPK_INV_SWEEP = 0, GPK_INV_CHAIN = 1, GPK_INV_CHAIN_AUG = 2, GPK_INV_BIG = 3 };
+int gpk_inverse_path(const gpk_handle* h, int32_t* path);
+/* The chain's workgroups wait on one another, so gpk_create uses it only when its grid fits the
+ * device's co-resident capacity (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs).  This
+ * overrides that capacity for handles created afterwards (workgroups > 0; 0 restores the device
+ * query) -- tests use it to force the per-sweep fallback. */
+int gpk_set_chain_capacity(int32_t workgroups);
+
 /* Graph selection state (see GPK_FLAG_NO_FAST_GRAPH): *fast = 1 if the next gpk_step uses the
  * fast graph, *rollbacks = batches rerun with the full graph so far.  Either pointer may be NULL. */
 int gpk_graph_mode(const gpk_handle* h, int32_t* fast, int64_t* rollbacks);
@@ -170,6 +181,11 @@ int gpk_loss_grad(gpk_handle* h, double* loss, double* grad_flat);
  * params and Adam state device-resident.  losses[n_steps] receives the loss evaluated
  * BEFORE each update (as step() returns it); may be NULL. */
 int gpk_step(gpk_handle* h, int32_t n_steps, double* losses);
+
+/* Capture and instantiate every step graph a gpk_step(n_steps) call can launch (full and fast,
+ * single-step and multi-step) without running a step: graph construction is a one-time host
+ * cost of the first call otherwise.  Params and Adam state are untouched. */
+int gpk_prepare(gpk_handle* h, int32_t n_steps);
 
 /* preds (model_GP_solver_2d.py:185-220 / model_GP_solver_1d.py:160-180) at the current
  * params: 2D out[m1*m2] (row-major, x-test indexes rows); 1D out[m1] (xte2 ignored). */

@@ -1,0 +1,42 @@
+"""bench.py's multi-GPU launcher on CPU (gloo, --dry-run stand-in solver, no GPU): `--gpus N`
+without a launcher starts N ranks of itself with the torch.distributed.run environment, the
+ranks form one process group (world N), and rank 0 prints ONE JSON line with n_gpus = N;
+launched by torch.distributed.run, --gpus must equal WORLD_SIZE."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tests.conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_n_spawns_n_ranks(n):
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--steps", "4", "--warmup", "1",
+                        "--dry-run"], env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n
+    assert out["steps"] == 4 and out["value"] > 0
+    assert "NOT a measurement" in out["data"]
+
+
+def test_gpus_must_match_world_size():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "2", "--dry-run"],
+                       env=_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE" in r.stderr

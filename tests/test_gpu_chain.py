@@ -85,5 +85,4 @@ def test_chain_aug_matches_gemm_form_and_oracle(name, dclass):
     assert np.max(np.abs(sa - sb) / np.abs(sb)) < 1e-8
     a.close()
     b.close()
-    if name != "c4":
-        _cmp_lossgrad(prob, params, Q, fs, flags=base)
+    _cmp_lossgrad(prob, params, Q, fs, flags=base)

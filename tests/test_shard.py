@@ -62,6 +62,37 @@ def test_group_loss_grad(eq, kind, n1, n2, nranks):
 
 
 @pytest.mark.gpu
+def test_group_eight_ranks_c4_size():
+    """Eight ranks (the MI355X node's GPU count) on the headline 256^2 problem (C4: Matern52_Cos,
+    Q = 30, seeded like the bench): loss and full gradient vs the oracle and vs one handle, then
+    5 Adam steps vs one handle."""
+    from tests.test_gpu_fullsize import _config_problem
+    prob, params, _, cfg = _config_problem("C4")
+    fs = cfg["freq_scale"]
+    g = _group(prob, 30, fs, 8)
+    s = device_solver(prob, 30, fs, flags=NO_AUG)
+    try:
+        assert g.shard_info()[1] == 8
+        g.set_params(params)
+        s.set_params(params)
+        lg, gg = g.loss_grad()
+        ls, gs = s.loss_grad()
+        lo, go = O.loss_grad_2d(prob, params)
+        tol = _tol(prob, params)
+        assert abs(lg - lo) / abs(lo) < tol, (lg, lo)
+        gd = O.unflatten_params(params, gg)
+        for k in go:
+            assert rel(O.flatten_params(gd[k]), O.flatten_params(go[k])) < tol, k
+        assert abs(lg - ls) / abs(ls) < 1e-11
+        assert rel(gg, gs) < 1e-9
+        assert rel(g.step(5), s.step(5)) < 1e-10
+        assert rel(g.get_flat(), s.get_flat()) < 1e-9
+    finally:
+        g.close()
+        s.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nranks,flags", [(2, 0), (4, 0), (2, 8)])
 def test_group_trajectory_matches_unsharded(nranks, flags):
     """10 Adam steps of the sharded group == 10 steps of one handle (params, losses); flags 8
