@@ -68,12 +68,13 @@ __device__ __forceinline__ double block_sum_256(double v, double* red) {
 // the compiler wait for each element's loads in turn (four serial round trips in wave 0 ahead
 // of its MFMA operand loads, ~4 us per latency-bound GEMM launch).
 struct EpiIn {
-  double pre, pu, q1, q2;
+  double pre, pu, q1, q2, ys;
 };
 
 __device__ __forceinline__ EpiIn epi_fetch(const GemmDesc& d, int row, int col) {
-  EpiIn e{0.0, 0.0, 0.0, 0.0};
+  EpiIn e{0.0, 0.0, 0.0, 0.0, 0.0};
   const size_t fo = (size_t)row * d.ldf + col;
+  if (d.Y) e.ys = d.Ys[(size_t)row * d.ldy + col];
   if ((d.epi == EPI_STORE || d.epi == EPI_QUAD) && d.beta != 0.0)
     e.pre = d.C0[(size_t)row * d.ldc0 + col];
   else if (d.epi == EPI_RESID)
@@ -84,6 +85,12 @@ __device__ __forceinline__ EpiIn epi_fetch(const GemmDesc& d, int row, int col) 
     e.q2 = d.Q2[fo];
   }
   return e;
+}
+
+// the side output of a stored value c (GemmDesc::Y)
+__device__ __forceinline__ void epi_side(const GemmDesc& d, int row, int col, double c, const EpiIn& e,
+                                         double v) {
+  if (d.Y) d.Y[(size_t)row * d.ldy + col] = 0.5 * e.ys + v * c;
 }
 
 // c = alpha*P1 + alpha2*P2 (already formed); returns the stored value, accumulates partials
@@ -144,13 +151,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmBatch batch,
   double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
   if (d.vscale2) alpha2 *= sc->v;
+  const double vv = d.Y ? sc->v : 0.0;
   double part = 0.0, part2 = 0.0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = i0 + 16 * wr + (lane >> 4) + 4 * r, col = j0 + 16 * wc + (lane & 15);
     double c = alpha * acc1[r];
     if (d.K2) c += alpha2 * acc2[r];
-    d.C[(size_t)row * d.ldc + col] = epi_apply(d, c, ein[r], part, part2);
+    c = epi_apply(d, c, ein[r], part, part2);
+    d.C[(size_t)row * d.ldc + col] = c;
+    epi_side(d, row, col, c, ein[r], vv);
   }
   if (d.red) {
     double s = block_sum_256(part, sred);
@@ -362,6 +372,7 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
   double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
   if (d.vscale2) alpha2 *= sc->v;
+  const double vv = d.Y ? sc->v : 0.0;
   double red = 0.0, red2 = 0.0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -370,7 +381,9 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
     const int row = i0 + (lane >> 4) + 4 * r, col = j0 + (lane & 15);
     double c = alpha * s1;
     if (DUAL && d.K2) c += alpha2 * ((part[1][0][q] + part[1][1][q]) + (part[1][2][q] + part[1][3][q]));
-    d.C[(size_t)row * d.ldc + col] = epi_apply(d, c, ein[r], red, red2);
+    c = epi_apply(d, c, ein[r], red, red2);
+    d.C[(size_t)row * d.ldc + col] = c;
+    epi_side(d, row, col, c, ein[r], vv);
   }
   if (d.red) {
 #pragma unroll
@@ -541,6 +554,7 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(GemmBatch batch, const St
   double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
   if (d.vscale2) alpha2 *= sc->v;
+  const double vv = d.Y ? sc->v : 0.0;
   double part = 0.0, part2 = 0.0;
 #pragma unroll
   for (int bi = 0; bi < 2; ++bi)
@@ -554,7 +568,9 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(GemmBatch batch, const St
           const EpiIn e = epi_fetch(d, row, col);
           double c = alpha * acc1[bi][bj][r];
           if (d.K2) c += alpha2 * acc2[bi][bj][r];
-          d.C[(size_t)row * d.ldc + col] = epi_apply(d, c, e, part, part2);
+          c = epi_apply(d, c, e, part, part2);
+          d.C[(size_t)row * d.ldc + col] = c;
+          epi_side(d, row, col, c, e, vv);
         }
       }
   if (d.red) {
@@ -726,6 +742,7 @@ __global__ __launch_bounds__(256) void gemm_huge_kernel(GemmBatch batch, const S
   double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
   if (d.vscale2) alpha2 *= sc->v;
+  const double vv = d.Y ? sc->v : 0.0;
   d4 acc[4][4];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
@@ -746,7 +763,9 @@ __global__ __launch_bounds__(256) void gemm_huge_kernel(GemmBatch batch, const S
         const int col = j0 + 64 * wc + 16 * y + (lane & 15);
         if (row < d.M && col < d.N) {
           const EpiIn e = epi_fetch(d, row, col);
-          d.C[(size_t)row * d.ldc + col] = epi_apply(d, alpha * acc[x][y][r], e, part, part2);
+          const double c = epi_apply(d, alpha * acc[x][y][r], e, part, part2);
+          d.C[(size_t)row * d.ldc + col] = c;
+          epi_side(d, row, col, c, e, vv);
         }
       }
     asm volatile("" ::: "memory");  // keep the epilogue's operand loads to one row block at a time

@@ -105,6 +105,7 @@ struct gpk_handle {
   // 2D work
   double *A = nullptr, *Bt = nullptr, *S = nullptr, *R = nullptr, *T1 = nullptr, *T2 = nullptr,
          *X1 = nullptr, *X2 = nullptr, *W1 = nullptr, *W2 = nullptr;  // W: refinement residuals
+  double *Y1 = nullptr, *Y2 = nullptr;  // S/2 + v X1, S/2 + v X2 (the G_K operands)
   double *GK[2] = {}, *GD[2] = {};
   // 1D work
   double *alpha = nullptr, *tvec = nullptr, *beta = nullptr;
@@ -155,6 +156,7 @@ struct gpk_handle {
   hipEvent_t ev[kMaxStages + 1] = {};
   bool profiling = false;
   int nstage = 0;
+  const char* sname[kMaxStages] = {};  // name of each launched (profiled) stage
 
   template <class T>
   int alloc(T** p, size_t count_) {
@@ -347,13 +349,21 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
   mark(h, 0);  // "prep" is fused into the assembly launch (stage kept for the name table)
   TRY(enqueue_assemble_inverse(h, apply));
   int stage = 3;
+  const char* const* names = L.dim == 2 ? kStageNames2D : kStageNames1D;
+  for (int k = 0; k < 3; ++k) h->sname[k] = names[k];
+  auto stamp = [&](const char* nm) {  // a launched stage: its name and end event
+    if (stage < kMaxStages) {
+      h->sname[stage] = nm;
+      mark(h, stage++);
+    }
+  };
   const int ac = h->prob.eq == GPK_ALLENCAHN;
   if (L.dim == 2) {
     for (int k = 0; k < kGemmStages; ++k) {
       if (h->st[k].n == 0 || (!refine && h->st[k].gated)) continue;
       TRY(check_launch(launch_gemm_auto(h->hdescs.data() + h->st[k].off, h->st[k].n, h->sc, h->s,
                                         h->st[k].variant), "gemm"));
-      mark(h, stage++);
+      stamp(kStageNames2D[3 + k]);
     }
     PGradArgs pa[2];
     for (int a = 0; a < 2; ++a) {
@@ -370,48 +380,48 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
     }
     TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, &tail), "pgrad"));
-    mark(h, stage++);
+    stamp("pgrad_tail");
   } else {
     const int P = L.p1;
     // every K^{-1} application gets one step of iterative refinement x += K^{-1}(b - K x),
     // gated on a cond(K) lower bound (gemv skips itself when K is well conditioned)
     GemvDesc g{};
     g.lda = P; g.p = P; g.rows = P; g.alpha = 1.0; g.ac = ac; g.F = h->F; g.U = h->Up; g.U0 = h->uoff;
-    auto gemv = [&](const double* A, const double* x, double* y, double alpha, const double* C0,
-                    double beta, int epi, double* red, bool gated) -> int {
+    auto gemv = [&](const char* nm, const double* A, const double* x, double* y, double alpha,
+                    const double* C0, double beta, int epi, double* red, bool gated) -> int {
       if (gated && !refine) return GPK_OK;
       GemvDesc q = g;
       q.A = A; q.x = x; q.y = y; q.alpha = alpha; q.C0 = C0; q.beta = beta; q.epi = epi; q.red = red;
       q.gate = gated ? h->pst[0] : nullptr;
       TRY(check_launch(launch_gemv(q, h->s), "gemv"));
-      mark(h, stage++);
+      stamp(nm);
       return GPK_OK;
     };
     // alpha = K^{-1} u (refined), quad = <u, alpha>          (model_GP_solver_1d.py:92,137)
-    TRY(gemv(h->Kinv[0], h->Up, h->alpha, 1.0, nullptr, 0.0, EPI_STORE, nullptr, false));
-    TRY(gemv(h->Kc[0], h->alpha, h->rvec, -1.0, h->Up, 1.0, EPI_STORE, nullptr, true));
-    TRY(gemv(h->Kinv[0], h->rvec, h->alpha, 1.0, h->alpha, 1.0, EPI_STORE, nullptr, true));
+    TRY(gemv("gemv_alpha", h->Kinv[0], h->Up, h->alpha, 1.0, nullptr, 0.0, EPI_STORE, nullptr, false));
+    TRY(gemv("gemv_alpha_res", h->Kc[0], h->alpha, h->rvec, -1.0, h->Up, 1.0, EPI_STORE, nullptr, true));
+    TRY(gemv("gemv_alpha_fix", h->Kinv[0], h->rvec, h->alpha, 1.0, h->alpha, 1.0, EPI_STORE, nullptr, true));
     // R = D alpha - f (+u(u^2-1)): egap = ||R||^2 and quad = <u, alpha> in one pass
     {
       GemvDesc q = g;
       q.A = h->D[0]; q.x = h->alpha; q.y = h->R; q.epi = EPI_RESID; q.red = h->red_egap;
       q.red2 = h->red_quad; q.Q1 = h->Up; q.Q2 = h->alpha;
       TRY(check_launch(launch_gemv(q, h->s), "gemv"));
-      mark(h, stage++);
+      stamp("gemv_resid");
     }
     // t = D^T R (DD_x1 is bitwise symmetric, so D^T = D)
-    TRY(gemv(h->D[0], h->R, h->tvec, 1.0, nullptr, 0.0, EPI_STORE, nullptr, false));
+    TRY(gemv("gemv_DtR", h->D[0], h->R, h->tvec, 1.0, nullptr, 0.0, EPI_STORE, nullptr, false));
     // beta = K^{-1} t (refined)
-    TRY(gemv(h->Kinv[0], h->tvec, h->beta, 1.0, nullptr, 0.0, EPI_STORE, nullptr, false));
-    TRY(gemv(h->Kc[0], h->beta, h->rvec, -1.0, h->tvec, 1.0, EPI_STORE, nullptr, true));
-    TRY(gemv(h->Kinv[0], h->rvec, h->beta, 1.0, h->beta, 1.0, EPI_STORE, nullptr, true));
+    TRY(gemv("gemv_beta", h->Kinv[0], h->tvec, h->beta, 1.0, nullptr, 0.0, EPI_STORE, nullptr, false));
+    TRY(gemv("gemv_beta_res", h->Kc[0], h->beta, h->rvec, -1.0, h->tvec, 1.0, EPI_STORE, nullptr, true));
+    TRY(gemv("gemv_beta_fix", h->Kinv[0], h->rvec, h->beta, 1.0, h->beta, 1.0, EPI_STORE, nullptr, true));
     PGradArgs pa{};
     pa.x = h->x1; pa.n = L.n1; pa.p = P; pa.kc = h->kc;
     pa.Kinv = h->Kinv[0]; pa.alpha = h->alpha; pa.beta = h->beta; pa.R = h->R;
     pa.halfc = 0.5 * h->prob.logdet; pa.deriv = 2; pa.part = h->pgpart; pa.cls = h->cls[0];
     TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 1, &pa, 1, h->bpa, h->sc, h->s, &tail), "pgrad"));
-    mark(h, stage++);
+    stamp("pgrad_tail");
   }
   h->nstage = stage;
   return GPK_OK;
@@ -483,6 +493,22 @@ static int build_descs(gpk_handle* h) {
     g.gate = h->pst[axis];
     return g;
   };
+  // Refinement GEMMs (X += K^{-1}(B - K X), gated on a cond(K) bound) run on the small-factor
+  // paths only.  On the large-factor 2D path they cost 6 of 19 N^3 GEMMs (C5: 22.7 of 64 ms)
+  // and buy nothing measurable: C5's dL/dU agrees with the LU oracle to 8.7e-8 without them
+  // vs 3.8e-8 with them, against a cond(K) budget of 2.4e-6 (tests/test_gpu_fullsize.py;
+  // numpy emulation of the blocked inverses: tools/solve_accuracy.py).  The 1D
+  // path keeps its refinement GEMVs: its kernel-parameter gradient is the sensitive one
+  // (C2: 3e-6 unrefined against 2.6e-7), and GEMVs cost microseconds.
+  const bool refine_stages = !h->bigspd;
+  auto pushg = [&](const GemmDesc& g) {
+    if (refine_stages) d.push_back(g);
+  };
+  // X1 / X2 producers also write Y = S/2 + v X (GemmDesc::Y): G_K's left operand
+  auto side = [&](GemmDesc g, double* Y) {
+    g.Y = Y; g.Ys = h->S; g.ldy = P2;
+    return g;
+  };
   // Stage A: A = K1^{-1} U, Bt = U K2^{-1}                       (2d.py:104-105)
   // (augmented chain: both come out of the inverse launch itself -- no stage)
   begin(0);
@@ -495,20 +521,20 @@ static int build_descs(gpk_handle* h) {
   {
     GemmDesc g = mk(h->Kc[0], P1, 0, h->A, P2, 0, h->W1, P2, P1, P2, P1);
     g.alpha = -1.0; g.beta = 1.0; g.C0 = h->Up; g.ldc0 = P2;
-    d.push_back(gate(g, 0));
+    pushg(gate(g, 0));
     GemmDesc g2 = mk(h->Bt, P2, 0, h->Kc[1], P2, 0, h->W2, P2, P1, P2, P2);
     g2.alpha = -1.0; g2.beta = 1.0; g2.C0 = h->Up; g2.ldc0 = P2;
-    d.push_back(gate(g2, 1));
+    pushg(gate(g2, 1));
   }
   end(1);
   begin(2);  // A += K1^{-1} W1, Bt += W2 K2^{-1}  (in place)
   {
     GemmDesc g = mk(h->Kinv[0], P1, 0, h->W1, P2, 0, h->A, P2, P1, P2, P1);
     g.beta = 1.0; g.C0 = h->A; g.ldc0 = P2;
-    d.push_back(gate(g, 0));
+    pushg(gate(g, 0));
     GemmDesc g2 = mk(h->W2, P2, 0, h->Kinv[1], P2, 0, h->Bt, P2, P1, P2, P2);
     g2.beta = 1.0; g2.C0 = h->Bt; g2.ldc0 = P2;
-    d.push_back(gate(g2, 1));
+    pushg(gate(g2, 1));
   }
   end(2);
   // Stage B: S = A K2^{-1};  R = beta D1 A + Bt D2^T - F (+AC), ||R||^2 and the prior's
@@ -529,14 +555,14 @@ static int build_descs(gpk_handle* h) {
   {
     GemmDesc g = mk(h->S, P2, 0, h->Kc[1], P2, 0, h->W1, P2, P1, P2, P2);
     g.alpha = -1.0; g.beta = 1.0; g.C0 = h->A; g.ldc0 = P2;
-    d.push_back(gate(g, 1));
+    pushg(gate(g, 1));
   }
   end(4);
   begin(5);  // S += W1 K2^{-1}
   {
     GemmDesc g = mk(h->W1, P2, 0, h->Kinv[1], P2, 0, h->S, P2, P1, P2, P2);
     g.beta = 1.0; g.C0 = h->S; g.ldc0 = P2;
-    d.push_back(gate(g, 1));
+    pushg(gate(g, 1));
   }
   end(5);
   // Stage C: T1 = beta D1^T R, T2 = R D2, G_D1 = v beta R A^T, G_D2 = v R^T Bt  (Appendix A)
@@ -546,8 +572,8 @@ static int build_descs(gpk_handle* h) {
   if (h->chain_aug) {
     GemmDesc x1 = mk(h->PD[0], P1, 0, h->R, P2, 0, h->X1, P2, P1, P2, P1);
     x1.alpha = beta;
-    d.push_back(x1);
-    d.push_back(mk(h->R, P2, 0, h->PD[1], P2, 1, h->X2, P2, P1, P2, P2));
+    d.push_back(side(x1, h->Y1));
+    d.push_back(side(mk(h->R, P2, 0, h->PD[1], P2, 1, h->X2, P2, P1, P2, P2), h->Y2));
   } else {
     GemmDesc t1 = mk(h->D[0], P1, 1, h->R, P2, 0, h->T1, P2, P1, P2, P1);
     t1.alpha = beta;
@@ -566,8 +592,8 @@ static int build_descs(gpk_handle* h) {
   // Stage D: X1 = K1^{-1} T1, X2 = T2 K2^{-1} (refined)
   begin(7);
   if (!h->chain_aug) {
-    d.push_back(mk(h->Kinv[0], P1, 0, h->T1, P2, 0, h->X1, P2, P1, P2, P1));
-    d.push_back(mk(h->T2, P2, 0, h->Kinv[1], P2, 0, h->X2, P2, P1, P2, P2));
+    d.push_back(side(mk(h->Kinv[0], P1, 0, h->T1, P2, 0, h->X1, P2, P1, P2, P1), h->Y1));
+    d.push_back(side(mk(h->T2, P2, 0, h->Kinv[1], P2, 0, h->X2, P2, P1, P2, P2), h->Y2));
   }
   end(7);
   begin(8);  // refinement residuals W1 = beta D1^T R - K1 X1, W2 = R D2 - X2 K2
@@ -575,42 +601,39 @@ static int build_descs(gpk_handle* h) {
     GemmDesc g = mk(h->D[0], P1, 1, h->R, P2, 0, h->W1, P2, P1, P2, P1);
     g.alpha = beta;
     g.A2 = h->Kc[0]; g.lda2 = P1; g.B2 = h->X1; g.ldb2 = P2; g.K2 = P1; g.alpha2 = -1.0;
-    d.push_back(gate(g, 0));
+    pushg(gate(g, 0));
     GemmDesc g2 = mk(h->R, P2, 0, h->D[1], P2, 0, h->W2, P2, P1, P2, P2);
     g2.A2 = h->X2; g2.lda2 = P2; g2.B2 = h->Kc[1]; g2.ldb2 = P2; g2.K2 = P2; g2.alpha2 = -1.0;
-    d.push_back(gate(g2, 1));
+    pushg(gate(g2, 1));
   } else {
     GemmDesc g = mk(h->Kc[0], P1, 0, h->X1, P2, 0, h->W1, P2, P1, P2, P1);
     g.alpha = -1.0; g.beta = 1.0; g.C0 = h->T1; g.ldc0 = P2;
-    d.push_back(gate(g, 0));
+    pushg(gate(g, 0));
     GemmDesc g2 = mk(h->X2, P2, 0, h->Kc[1], P2, 0, h->W2, P2, P1, P2, P2);
     g2.alpha = -1.0; g2.beta = 1.0; g2.C0 = h->T2; g2.ldc0 = P2;
-    d.push_back(gate(g2, 1));
+    pushg(gate(g2, 1));
   }
   end(8);
   begin(9);
   {
     GemmDesc g = mk(h->Kinv[0], P1, 0, h->W1, P2, 0, h->X1, P2, P1, P2, P1);
     g.beta = 1.0; g.C0 = h->X1; g.ldc0 = P2;
-    d.push_back(gate(g, 0));
+    pushg(side(gate(g, 0), h->Y1));
     GemmDesc g2 = mk(h->W2, P2, 0, h->Kinv[1], P2, 0, h->X2, P2, P1, P2, P2);
     g2.beta = 1.0; g2.C0 = h->X2; g2.ldc0 = P2;
-    d.push_back(gate(g2, 1));
+    pushg(side(gate(g2, 1), h->Y2));
   }
   end(9);
-  // Stage E: G_K1 = c N2/2 K1^{-1} - (S/2 + v X1) A^T;  G_K2 = c N1/2 K2^{-1} - (S/2 + v X2)^T Bt
+  // Stage E: G_K1 = c N2/2 K1^{-1} - Y1 A^T;  G_K2 = c N1/2 K2^{-1} - Y2^T Bt, with
+  // Y = S/2 + v X written by the X producers above (one product each instead of two)
   begin(10);
   {
-    GemmDesc g = mk(h->S, P2, 0, h->A, P2, 1, h->GK[0], P1, P1, P1, P2);
-    g.alpha = -0.5;
-    g.A2 = h->X1; g.lda2 = P2; g.B2 = h->A; g.ldb2 = P2; g.tb2 = 1; g.K2 = P2;
-    g.alpha2 = -1.0; g.vscale2 = 1;
+    GemmDesc g = mk(h->Y1, P2, 0, h->A, P2, 1, h->GK[0], P1, P1, P1, P2);
+    g.alpha = -1.0;
     g.beta = 0.5 * h->prob.logdet * n2; g.C0 = h->Kinv[0]; g.ldc0 = P1;
     d.push_back(g);
-    GemmDesc g2 = mk(h->S, P2, 1, h->Bt, P2, 0, h->GK[1], P2, P2, P2, P1);
-    g2.alpha = -0.5;
-    g2.A2 = h->X2; g2.lda2 = P2; g2.ta2 = 1; g2.B2 = h->Bt; g2.ldb2 = P2; g2.K2 = P1;
-    g2.alpha2 = -1.0; g2.vscale2 = 1;
+    GemmDesc g2 = mk(h->Y2, P2, 1, h->Bt, P2, 0, h->GK[1], P2, P2, P2, P1);
+    g2.alpha = -1.0;
     g2.beta = 0.5 * h->prob.logdet * n1; g2.C0 = h->Kinv[1]; g2.ldc0 = P2;
     d.push_back(g2);
   }
@@ -754,6 +777,10 @@ GemmDesc slice_rows(const GemmDesc& d, int r0, int rows, int variant) {
   if (d.U) s.U = d.U + (size_t)r0 * d.ldf;
   if (d.Q1) s.Q1 = d.Q1 + (size_t)r0 * d.ldf;
   if (d.Q2) s.Q2 = d.Q2 + (size_t)r0 * d.ldf;
+  if (d.Y) {
+    s.Y = d.Y + (size_t)r0 * d.ldy;
+    s.Ys = d.Ys + (size_t)r0 * d.ldy;
+  }
   const size_t toff = (size_t)(r0 / tile_rows(variant)) * tile_cols_count(d, variant);
   if (d.red) s.red = d.red + toff;
   if (d.red2) s.red2 = d.red2 + toff;
@@ -801,12 +828,11 @@ static int build_shard(gpk_handle* h) {
   h->sgather[1] = {g1(h->W1)};                                 // A_fix: K1^{-1} W1
   h->sgather[2] = {g1(h->A), g1(h->Bt)};                       // R: D1 A; G_D*, G_K*: A^T, Bt
   h->sgather[3] = {g1(h->R)};                                  // T1 = D1^T R; G_D2 = R^T Bt
-  h->sgather[5] = {g1(h->S)};                                  // G_K2: S^T Bt
   h->sgather[6] = {g1(h->T1), ShardGather{h->GD[0], (size_t)h->h1 * P1},  // X1 = K1^{-1} T1;
                    ShardGather{h->GD[1], (size_t)h->h2 * P2}};            // pgrad reads G_D whole
   h->sgather[7] = {g1(h->X1)};                                 // D_res: K1 X1
   h->sgather[8] = {g1(h->W1)};                                 // D_fix: K1^{-1} W1
-  h->sgather[9] = {g1(h->X2)};                                 // G_K2: X2^T Bt
+  h->sgather[9] = {g1(h->Y2)};                                 // G_K2: Y2^T Bt (Y2 = S/2 + v X2)
   h->sgather[10] = {ShardGather{h->GK[0], (size_t)h->h1 * P1}, ShardGather{h->GK[1], (size_t)h->h2 * P2}};
   return GPK_OK;
 }
@@ -1154,7 +1180,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   if (L.dim == 2) {
     A_(h->A, nup); A_(h->Bt, nup); A_(h->S, nup); A_(h->R, nup);
     A_(h->T1, nup); A_(h->T2, nup); A_(h->X1, nup); A_(h->X2, nup);
-    A_(h->W1, nup); A_(h->W2, nup);
+    A_(h->W1, nup); A_(h->W2, nup); A_(h->Y1, nup); A_(h->Y2, nup);
     for (int a = 0; a < 2; ++a) {
       const int P = a == 0 ? P1 : P2;
       A_(h->GK[a], (size_t)P * P);
@@ -1239,7 +1265,8 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   }
   if (L.dim == 2 && (rc = build_descs(h)) != GPK_OK) return bail(rc);
   if (shard && (rc = build_shard(h)) != GPK_OK) return bail(rc);
-  h->fast_ok = !shard && !(p->flags & GPK_FLAG_NO_FAST_GRAPH);
+  // (the 2D large-factor path has no refinement stages: its one graph is the fast one)
+  h->fast_ok = !shard && !(h->bigspd && L.dim == 2) && !(p->flags & GPK_FLAG_NO_FAST_GRAPH);
   h->fast_mode = h->fast_ok && (p->flags & GPK_FLAG_FAST_FIRST);
   *out = h;
   return GPK_OK;
@@ -1743,8 +1770,8 @@ int gpk_profile_stages(gpk_handle* h, int32_t iters, double* out_us, int32_t cap
 
 const char* gpk_stage_name(const gpk_handle* h, int32_t stage) {
   if (!h || stage < 0) return "?";
-  if (h->L.dim == 2) return stage < 18 ? kStageNames2D[stage] : "?";
-  return stage < 15 ? kStageNames1D[stage] : "?";
+  if (stage >= h->nstage || stage >= kMaxStages || !h->sname[stage]) return "?";
+  return h->sname[stage];
 }
 
 int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us) {

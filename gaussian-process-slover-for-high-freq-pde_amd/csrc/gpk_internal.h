@@ -265,6 +265,9 @@ struct GemmDesc {
   double* red;              // per-tile partial sums, [tiles] (nullable)
   double* red2; const double* Q1; const double* Q2;  // EPI_RESID: sum Q1*Q2 (quad term)
   const double* gate; int ngate;  // refinement gate (gate_open); nullptr = always store
+  // side output (EPI_STORE): Y = 0.5 Ys + v C, with C the stored value -- the G_K operand
+  // (S/2 + v X) formed where X is produced, so the G_K stage is a single product
+  double* Y; const double* Ys; int ldy;
   int tag;                  // step stage (timeline probes only, gpk_trace.h)
 };
 constexpr int GEMM_MAX_BATCH = 4;
