@@ -123,6 +123,7 @@ struct gpk_handle {
   unsigned int* aflag[2] = {};        // assembly -> pivot-0 hand-off counters (small path) /
                                       // update -> pivot hand-off counters (large path)
   bool bigspd = false;                // large-factor SPD inverse (spdinv_big.hip)
+  bool bigwide = false;               // ... with 128-wide sweeps
   bool chain = false;                 // small factors: persistent one-launch inverse (chain_kernel)
   bool chain_aug = false;             // ... which also solves A, Bt^T and K^{-1} D^T (2D, unsharded)
   unsigned int* cflags[2] = {};       // its hand-off flags [T*(T+taug) + 2T + 1] per factor
@@ -225,6 +226,7 @@ static void fill_spd(gpk_handle* h, SpdArgs* sa) {
     sa[a].status = h->status;
     sa[a].pst = h->pst[a];
     sa[a].flag = h->aflag[a];
+    sa[a].wide = h->bigwide ? 1 : 0;
   }
 }
 
@@ -1106,6 +1108,8 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     const int pmax = std::max(L.p1, L.dim == 2 ? L.p2 : 0);
     h->bigspd = (p->flags & GPK_FLAG_FORCE_BIG_SPD) != 0 ||
                 (!(p->flags & GPK_FLAG_FORCE_SMALL_SPD) && pmax >= SPD_BIG_MIN);
+    h->bigwide = h->bigspd && !(p->flags & GPK_FLAG_FORCE_NARROW_SPD) &&
+                 ((p->flags & GPK_FLAG_FORCE_WIDE_SPD) || pmax >= SPD_WIDE_MIN);
     // The persistent chain inverse needs its whole grid co-resident: the grid (workgroups of
     // every factor's row, the widest row times the factors) must fit the device's capacity for
     // the chain variant the step launches (occupancy per CU x CUs, so a CU-partitioned device
@@ -1165,7 +1169,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     A_(h->K[a], (size_t)P * P);
     A_(h->Kb[a], (size_t)P * P);
     A_(h->D[a], (size_t)P * P);
-    A_(h->piv[a], std::max<size_t>((size_t)P * 32, 64 * 64));  // large path: 64x64 L^{-1}
+    A_(h->piv[a], spd_big_piv_doubles(P));  // large path: W x W L^{-1} + 128-pivot scratch
     A_(h->ldet[a], P / 32);
     A_(h->Kc[a], (size_t)P * P);
     A_(h->pst[a], 2);
@@ -1615,6 +1619,12 @@ int gpk_class_count(const gpk_handle* h, int32_t axis, int32_t* ncls) {
   return GPK_OK;
 }
 
+int gpk_set_spd_big_workgroups(int32_t workgroups) {
+  if (workgroups < 0) return fail(GPK_EINVAL, "workgroups must be >= 0");
+  spd_big_set_workgroups(workgroups);
+  return GPK_OK;
+}
+
 int gpk_set_chain_capacity(int32_t workgroups) {
   g_chain_cap.store(workgroups > 0 ? workgroups : 0);
   return GPK_OK;
@@ -1622,7 +1632,7 @@ int gpk_set_chain_capacity(int32_t workgroups) {
 
 int gpk_inverse_path(const gpk_handle* h, int32_t* path) {
   if (!h || !path) return fail(GPK_EINVAL, "NULL argument");
-  *path = h->bigspd ? GPK_INV_BIG : h->chain_aug ? GPK_INV_CHAIN_AUG : h->chain ? GPK_INV_CHAIN : GPK_INV_SWEEP;
+  *path = h->bigspd ? (h->bigwide ? GPK_INV_BIG_WIDE : GPK_INV_BIG) : h->chain_aug ? GPK_INV_CHAIN_AUG : h->chain ? GPK_INV_CHAIN : GPK_INV_SWEEP;
   return GPK_OK;
 }
 
@@ -1996,7 +2006,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     // n^3 per factor over its ceil(p/64) sweeps; HBM: read + write the lower triangle
     for (int a = 0; a < L.naxes; ++a) {
       const double n = a == 0 ? n1 : n2;
-      flops += n * n * n / spd_big_sweeps(a == 0 ? L.p1 : L.p2);
+      flops += n * n * n / spd_big_sweeps(a == 0 ? L.p1 : L.p2, h->bigwide);
       bytes += 8.0 * n * n;
     }
     *avg_us = tot / iters;
@@ -2012,7 +2022,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     launch = [&]() { return launch_spd_big_tiles(sa, L.naxes, 0, h->s); };
     for (int a = 0; a < L.naxes; ++a) {
       const double n = a == 0 ? n1 : n2;
-      flops += n * n * n / spd_big_sweeps(a == 0 ? L.p1 : L.p2);
+      flops += n * n * n / spd_big_sweeps(a == 0 ? L.p1 : L.p2, h->bigwide);
       bytes += 8.0 * n * n;
     }
   } else if ((nm == "spd_pivot" || nm == "spd_panel") && h->bigspd) {

@@ -163,6 +163,7 @@ struct SpdArgs {
   double* pst;     // refinement gate [2]: K_00, bits of max diag K^{-1} (gate_open)
   int* status;     // nonzero => not positive definite
   unsigned int* flag;  // large path: update -> pivot hand-off counter (zero-initialised)
+  int wide;        // large path: 128-wide sweeps (else 64)
 };
 // Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.
 // pivot0_done: pivot block 0 was already factored (by the assembly launch).
@@ -225,16 +226,23 @@ __host__ __device__ inline int chain_role(int m, int x, int T, int TC) {
 hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s,
                             const PrepArgs* prep = nullptr, int q = 0);
 
-// Large-factor path (spdinv_big.hip): 64-wide pivots, panel + lower-tile MFMA update per sweep,
-// next pivot factored inside the update launch.  In place: K^{-1} ends in X.  Y is used as the
-// 64 x p panel buffer and piv as the 64 x 64 L^{-1} buffer (p >= 128).
-// Chosen when the largest padded factor is >= SPD_BIG_MIN (or forced by a problem flag).
+// Large-factor path (spdinv_big.hip): 64- or 128-wide pivots (SpdArgs::wide), panel + lower-tile
+// MFMA update per sweep, next pivot factored inside the update launch.  In place: K^{-1} ends in
+// X.  Y is used as the W x p panel buffer and piv as the W x W L^{-1} buffer + the 128-pivot's
+// scratch (spd_big_piv_doubles).
+// Chosen when the largest padded factor is >= SPD_BIG_MIN (or forced by a problem flag); the
+// 128-wide sweeps from SPD_WIDE_MIN (or forced).
 constexpr int SPD_BIG_MIN = 1600;
+constexpr int SPD_WIDE_MIN = 3072;
+size_t spd_big_piv_doubles(int p);
+// tile workgroups per factor of the update launch (0: two per CU); tests use a few to get long
+// runs of tiles per workgroup at small sizes
+void spd_big_set_workgroups(int g);
 hipError_t launch_spd_inverse_big(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
 // stage -1: pivot 0; 2k: panel of sweep k; 2k+1: update of sweep k
 hipError_t launch_spd_big_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
 hipError_t launch_spd_big_tiles(SpdArgs* args, int nmat, int k, hipStream_t s);  // bench only
-int spd_big_sweeps(int p);
+int spd_big_sweeps(int p, int wide);
 
 // Iterative-refinement gate: a refinement GEMM/GEMV runs only when the factor's condition
 // number may be large.  gate[0] = K_00 = max diagonal of K (written with pivot block 0),

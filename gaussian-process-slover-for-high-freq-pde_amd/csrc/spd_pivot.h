@@ -52,7 +52,9 @@ struct NoPivotHook {
   __device__ void pre() {}
   __device__ void post() {}
 };
-template <int BS = 4, typename LP = double*, typename Hook = NoPivotHook>
+// UNROLL: the 8 block steps unrolled (the chain's pivot: constant LDS offsets) or kept as a loop
+// (1: a quarter of the registers, for kernels that must stay at two waves per SIMD)
+template <int BS = 4, typename LP = double*, typename Hook = NoPivotHook, int UNROLL = 8>
 __device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t, int* status,
                                                        Hook hook = Hook()) {
   static_assert(BS == 4, "the MFMA update is rank 4");
@@ -72,7 +74,7 @@ __device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t,
   const double s0 = lk == 0 ? 1.0 : 0.0, s1 = lk == 1 ? 1.0 : 0.0, s2 = lk == 2 ? 1.0 : 0.0,
                s3 = lk == 3 ? 1.0 : 0.0;
   __syncthreads();
-#pragma unroll
+#pragma unroll UNROLL
   for (int kb = 0; kb < 8; ++kb) {
     const int b0 = 4 * kb;
     double D[4][4], ar[4], ac[4], mb[4];

@@ -5,45 +5,58 @@
 // code/model_GP_solver_advection.py:104-105,153-158): X <- K^{-1} in place, log det K per 32-row
 // block, refinement gate, non-PD status.  The 32-wide sweep of spdinv.hip re-reads and rewrites
 // the whole matrix once per 32 columns and recomputes its panel in every tile; at p >= ~1024
-// that is HBM- and launch-bound.  This path sweeps 64-wide pivot blocks and splits each sweep
-// into three pieces of work:
+// that is HBM- and launch-bound.  This path sweeps W = 64 R wide pivot blocks (R = 1 or 2) over
+// 64 x 64 tiles and splits each sweep into three pieces of work:
 //
-//   panel   Z = L^{-1} X_{P,:}   (64 x p, one small MFMA GEMM per 64-column block; Z_P = L^{-1})
+//   panel   Z = L^{-1} X_{P,:}   (W x p, small MFMA GEMMs per 64-column block; Z_P = L^{-1})
 //   update  X_IJ <- s_IJ (base_IJ - Z_I^T Z_J) on the LOWER tiles only (I >= J), in place:
-//             I,J != P : X_IJ - Z_I^T Z_J          (Schur complement, the SYRK-shaped bulk)
-//             one of I,J == P : + Z_I^T Z_J        (= L^{-T} V: the swept panel)
-//             I = J = P : - Z_P^T Z_P              (= -S^{-1})
-//   pivot   the next pivot block S = X_{k+1,k+1} is factored (Cholesky + L^{-1}, in LDS) by one
-//           extra workgroup of the update launch, right after the workgroup that owns that tile
-//           has written it back (release + counter hand-off, MI355X_MICROARCH inter-workgroup
-//           visibility), so the serial pivot chain runs under the bulk of the update.
+//             I,J not in P : X_IJ - Z_I^T Z_J          (Schur complement, the SYRK-shaped bulk)
+//             one of I,J in P : + Z_I^T Z_J           (= L^{-T} V: the swept panel)
+//             I, J in P : - Z_I^T Z_J                 (= -S^{-1})
+//   pivot   the next pivot block S = X_{k+1,k+1} (W x W) is factored (Cholesky + L^{-1}) by one
+//           extra workgroup of the update launch, right after the workgroups that own its
+//           tiles have written them back (write-through stores + counter hand-off, MI355X_MICROARCH
+//           inter-workgroup visibility), so the serial pivot chain runs under the bulk of the update.
 //
-// After T = ceil(p/64) sweeps X = -K^{-1}; the last sweep flips the sign, mirrors every lower
-// tile into the upper triangle (LDS transpose, coalesced stores) and publishes max diag K^{-1}
-// for the refinement gate.  Flops: p^3 (potrf + potri equivalent), all on v_mfma_f64_16x16x4.
+// After ceil(p/W) sweeps X = -K^{-1}; the last sweep flips the sign, mirrors every lower tile into
+// the upper triangle (LDS transpose, coalesced stores) and publishes max diag K^{-1} for the
+// refinement gate.  Flops: p^3 (potrf + potri equivalent), all on v_mfma_f64_16x16x4.
+//
+// Sweep width.  Per sweep the update reads and writes the lower triangle once (8 p^2 B) for
+// W p^2 flops, i.e. W / 8 flop per byte of X traffic: at W = 64 the 4096^2 update is bound by the
+// matrix traffic (~20 TF/s), at W = 128 (R = 2) by MFMA.  Wide sweeps need a 128-pivot; its
+// factorisation is exposed where the update is short, so R = 2 is used for the largest factors
+// only (SPD_WIDE_MIN) and R = 1 keeps the shorter serial chain at ~2048.
 // The 64-pivot factorisation is two 32-pivots (spd_pivot.h) glued by three 32x32 MFMA products:
 //   L11^{-1} = chol_inv(S11);  V = L11^{-1} S12;  L22^{-1} = chol_inv(S22 - V^T V);
-//   (L^{-1})_21 = -L22^{-1} V^T L11^{-1}.
+//   (L^{-1})_21 = -L22^{-1} V^T L11^{-1};
+// the 128-pivot is the same recursion one level up with 64-pivots and 64x64 products.
+#include <atomic>
+
 #include "gpk_internal.h"
 #include "spd_pivot.h"
 
 namespace gpk {
 
+static std::atomic<int> g_big_wgs{0};  // spd_big_set_workgroups override (tests)
+void spd_big_set_workgroups(int g) { g_big_wgs.store(g > 0 ? g : 0); }
+
 namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
-constexpr int BW = 64;   // pivot / tile width
+constexpr int BW = 64;   // tile width (and the 64-pivot)
 constexpr int SS = 65;   // 64x64 LDS tile stride (doubles)
 
 struct BigSpdBatch {
   double* X[2];      // the matrix, inverted in place
-  double* Z[2];      // [64][p] panel
-  double* Li[2];     // [64][64] L^{-1} of the current pivot block (row-major, zero upper)
+  double* Z[2];      // [W][p] panel
+  double* Li[2];     // [W][W] L^{-1} of the current pivot block (row-major, zero upper) + scratch
   double* ldet[2];   // [p/32]
   double* pst[2];    // refinement gate [2]
   int* status[2];
   unsigned int* flag[2];
-  int p[2], n[2], T[2];
+  int p[2], n[2], T[2];  // T: 64-wide tiles per dimension
+  int G;                 // tile workgroups per factor in the update launch
 };
 
 __device__ __forceinline__ int bw(int p, int I) { return min(BW, p - BW * I); }
@@ -60,6 +73,24 @@ __device__ __forceinline__ d4 mma16(const double* a, int sai, int sak, const dou
                                                b[k * sbk + (j0 + li) * sbj], acc, 0, 0, 0);
   }
   return acc;
+}
+
+// this wave's 32x32 quadrant (wr, wc) of a 64x64x64 product out of LDS (2x2 blocks of 16x16):
+// element (32wr + 16bi + (lane>>4) + 4r, 32wc + 16bj + (lane&15)) in acc[bi][bj][r]
+__device__ __forceinline__ void mm64(const double* a, int sai, int sak, const double* b, int sbk, int sbj,
+                                     int wr, int wc, int lane, d4 (&acc)[2][2]) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < 64; k0 += 32)
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+        acc[bi][bj] = mma16(a + k0 * sak, sai, sak, b + k0 * sbk, sbk, sbj, 32 * wr + 16 * bi,
+                            32 * wc + 16 * bj, lane, acc[bi][bj]);
 }
 
 // S[r][c] = src[r*ld + c] for r < h, c < w (else 0): 64x64 tile, all 16 loads per thread in
@@ -89,16 +120,18 @@ __device__ __forceinline__ void load_tile_t(double* S, const double* src, int ld
   for (int q = 0; q < 16; ++q) S[r * SS + c0 + 4 * q] = v[q];
 }
 
-// the 32-pivot factorisation as a real call: inlined twice (or in a loop) its fully unrolled
-// register blocking blows past 256 VGPRs and spills; as a callee it keeps its own ~130
-__device__ __noinline__ double pivot32(lds_ptr A, lds_ptr M, lds_ptr pv, int t, int* status) {
-  return pivot_chol_inv_block<4, lds_ptr>(A, M, pv, t, status);
+// the 32-pivot factorisation with its 8 block steps kept as a loop: inlined, it stays within
+// the update kernel's two-waves-per-SIMD register budget (a call costs the ABI's saved
+// registers: 277 VGPR + AGPR, one wave per SIMD)
+__device__ __forceinline__ double pivot32(double* A, double* M, double* pv, int t, int* status) {
+  return pivot_chol_inv_block<4, double*, NoPivotHook, 1>(A, M, pv, t, status);
 }
 
-// Factor the w x w (w = 32 or 64) diagonal block kb of X (symmetric; both triangles valid):
-// writes Li (64x64 row-major, zero-padded), ldet[2kb(+1)], status.  One 256-thread workgroup.
-__device__ void pivot64(const double* X, int p, int kb, double* Li, double* ldet, int* status,
-                        double* sm) {
+// Factor the w x w (w = 32 or 64) SPD block at src (leading dimension ld; both triangles valid):
+// writes its L^{-1} as a 64x64 block at Li (leading dimension ldl, zero-padded), ldet2[0..1]
+// (one entry per 32 rows), status.  One 256-thread workgroup; sm >= PIVOT_LDS doubles.
+__device__ __forceinline__ void pivot64(const double* src, int ld, int w, double* Li, int ldl, double* ldet2,
+                        int* status, double* sm) {
   double* S = sm;                   // [64][SS]
   double* A = S + 64 * SS;          // [32][SP] factor scratch, then W
   double* M1 = A + 32 * SP;         // [32][SP]
@@ -107,9 +140,7 @@ __device__ void pivot64(const double* X, int p, int kb, double* Li, double* ldet
   double* pv = V + 32 * SP;         // [32]
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  const int w = bw(p, kb);
-  const double* Xs = X + (size_t)(BW * kb) * p + BW * kb;
-  load_tile(S, Xs, p, w, w, t);
+  load_tile(S, src, ld, w, w, t);
   __syncthreads();
   for (int e = t; e < 1024; e += 256) A[(e >> 5) * SP + (e & 31)] = S[(e >> 5) * SS + (e & 31)];
   __syncthreads();
@@ -120,7 +151,7 @@ __device__ void pivot64(const double* X, int p, int kb, double* Li, double* ldet
   // moved to M1), h = 1 the Schur complement S22 - V^T V of the second half
 #pragma nounroll
   for (int h = 0; h < w / 32; ++h) {
-    ls[h] = pivot32((lds_ptr)A, (lds_ptr)M2, (lds_ptr)pv, t, status);
+    ls[h] = pivot32(A, M2, pv, t, status);
     if (h == 0 && w == BW) {
       for (int e = t; e < 32 * SP; e += 256) M1[e] = M2[e];
       __syncthreads();
@@ -165,21 +196,113 @@ __device__ void pivot64(const double* X, int p, int kb, double* Li, double* ldet
     if (r < 32 && c < 32) v = M1[r * SP + c];
     else if (r >= 32 && r < w && c < 32) v = S[r * SS + c];
     else if (r >= 32 && r < w && c >= 32 && c < w) v = M2[(r - 32) * SP + c - 32];
-    Li[e] = v;
+    Li[r * ldl + c] = v;
   }
   if (t == 0) {
-    ldet[2 * kb] = ls1;
-    if (w == BW) ldet[2 * kb + 1] = ls2;
+    ldet2[0] = ls1;
+    if (w == BW) ldet2[1] = ls2;
   }
 }
 
 constexpr int PIVOT_LDS = 64 * SS + 4 * 32 * SP + 32;  // doubles
 
+// Factor the w x w (w <= 128) diagonal block at src: L^{-1} as a 128x128 block at Li (ld 128,
+// zero upper / padding), ldet4[0..3], status.  Li + 128*128 holds two 64x64 scratch blocks (the
+// Schur complement, V).  Every intermediate goes through global memory (this workgroup's own
+// writes, read back after a barrier: one L1 per workgroup), so the LDS need is pivot64's.
+//   L11^{-1} = chol_inv(S11);  V = L11^{-1} S12;  L22^{-1} = chol_inv(S22 - V^T V);
+//   (L^{-1})_21 = -L22^{-1} (V^T L11^{-1})
+__device__ __forceinline__ void pivot128(const double* src, int ld, int w, double* Li, double* ldet4, int* status,
+                         double* sm) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  double* Sg = Li + 128 * 128;  // [64][64] Schur complement
+  double* Vg = Sg + 64 * 64;    // [64][64] V
+  const int w1 = min(BW, w), w2 = w - BW;
+  pivot64(src, ld, w1, Li, 128, ldet4, status, sm);
+  __syncthreads();
+  if (w2 <= 0) return;  // (the last, <= 64 wide sweep reads the L11 block only)
+  double* sA = sm;
+  double* sB = sm + 64 * SS;
+  d4 acc[2][2];
+  // V = L11^{-1} S12  (columns >= w2 are zero); S12 = S21^T from the lower storage (during the
+  // sweeps only the lower tiles are current)
+  load_tile(sA, Li, 128, BW, BW, t);
+  load_tile_t(sB, src + (size_t)BW * ld, ld, BW, w2, t);
+  __syncthreads();
+  mm64(sA, SS, 1, sB, SS, 1, wr, wc, lane, acc);
+  __syncthreads();
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 32 * wr + 16 * bi + (lane >> 4) + 4 * r, j = 32 * wc + 16 * bj + (lane & 15);
+        sA[i * SS + j] = acc[bi][bj][r];
+        Vg[i * 64 + j] = acc[bi][bj][r];
+      }
+  __syncthreads();
+  // Schur complement S22 - V^T V -> Sg
+  mm64(sA, 1, SS, sA, SS, 1, wr, wc, lane, acc);
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 32 * wr + 16 * bi + (lane >> 4) + 4 * r, j = 32 * wc + 16 * bj + (lane & 15);
+        if (i < w2 && j < w2) Sg[i * 64 + j] = src[(size_t)(BW + i) * ld + BW + j] - acc[bi][bj][r];
+      }
+  __syncthreads();
+  pivot64(Sg, 64, w2, Li + BW * 128 + BW, 128, ldet4 + 2, status, sm);
+  __syncthreads();
+  // W = V^T L11^{-1}, then (L^{-1})_21 = -L22^{-1} W
+  load_tile(sA, Vg, 64, BW, BW, t);
+  load_tile(sB, Li, 128, BW, BW, t);
+  __syncthreads();
+  mm64(sA, 1, SS, sB, SS, 1, wr, wc, lane, acc);
+  __syncthreads();
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        sA[(32 * wr + 16 * bi + (lane >> 4) + 4 * r) * SS + 32 * wc + 16 * bj + (lane & 15)] = acc[bi][bj][r];
+  load_tile(sB, Li + BW * 128 + BW, 128, BW, BW, t);
+  __syncthreads();
+  mm64(sB, SS, 1, sA, SS, 1, wr, wc, lane, acc);
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 32 * wr + 16 * bi + (lane >> 4) + 4 * r, j = 32 * wc + 16 * bj + (lane & 15);
+        Li[(BW + i) * 128 + j] = -acc[bi][bj][r];
+        Li[i * 128 + BW + j] = 0.0;  // upper-right block
+      }
+}
+
+// the pivot block of sweep k: 64-pivot (R = 1) or 128-pivot (R = 2)
+template <int R>
+__device__ __forceinline__ void pivot_block(const BigSpdBatch& b, int m, int k, double* sm) {
+  const int p = b.p[m];
+  const int r0 = BW * R * k, w = min(BW * R, p - r0);
+  const double* src = b.X[m] + (size_t)r0 * p + r0;
+  if (R == 1)
+    pivot64(src, p, w, b.Li[m], BW, b.ldet[m] + 2 * k, b.status[m], sm);
+  else
+    pivot128(src, p, w, b.Li[m], b.ldet[m] + 4 * k, b.status[m], sm);
+}
+
+template <int R>
 __global__ __launch_bounds__(256) void big_pivot_init_kernel(BigSpdBatch b) {
   const int m = blockIdx.x;
   __shared__ double sm[PIVOT_LDS];
   const double x00 = b.X[m][0];
-  pivot64(b.X[m], b.p[m], 0, b.Li[m], b.ldet[m], b.status[m], sm);
+  pivot_block<R>(b, m, 0, sm);
   if (threadIdx.x == 0) {
     b.pst[m][0] = x00;   // K_00 = max diag K (stationary kernel + jitter)
     b.pst[m][1] = 0.0;   // max diag K^{-1}: atomicMax'd by the last sweep
@@ -187,44 +310,57 @@ __global__ __launch_bounds__(256) void big_pivot_init_kernel(BigSpdBatch b) {
   }
 }
 
-// Z[:, J-block] = L^{-1} X_{P,J}  (X_{P,J} of the lower storage: row block P for J < P, the
-// transpose of column block P for J > P);  Z[:, P-block] = L^{-1}.
+// Row block rh (64 rows) of the panel Z[:, J-block] = L^{-1} X_{P,J} (X_{P,J} of the lower
+// storage: row block P for J < P, the transpose of column block P for J > P); Z[:, P-block] =
+// L^{-1}.  L^{-1} is lower triangular: row block rh sums the column blocks kh <= rh.
+template <int R>
 __global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
-  const int m = blockIdx.y, J = blockIdx.x;
+  const int m = blockIdx.y, J = blockIdx.x / R, rh = blockIdx.x % R;
   const int p = b.p[m], T = b.T[m];
-  if (k >= T || J >= T) return;
+  const int P0 = R * k;  // first tile of the swept block
+  if (P0 >= T || J >= T) return;
+  const int w = min(BW * R, p - BW * P0);  // sweep width
+  if (BW * rh >= w) return;
+  const int hr = min(BW, w - BW * rh);     // rows of this output block
+  const int ldl = BW * R;
   const double* X = b.X[m];
   double* Z = b.Z[m];
   const double* Li = b.Li[m];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int wP = bw(p, k), wJ = bw(p, J);
-  if (J == k) {
-    for (int e = t; e < wP * wP; e += 256) {
-      const int r = e / wP, c = e - r * wP;
-      Z[(size_t)r * p + BW * k + c] = Li[r * BW + c];
+  const int wJ = bw(p, J);
+  if (J >= P0 && J < P0 + R) {
+    const int jc = J - P0;
+    for (int e = t; e < BW * BW; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      if (r < hr && c < wJ) Z[(size_t)(BW * rh + r) * p + BW * J + c] = Li[(BW * rh + r) * ldl + BW * jc + c];
     }
     return;
   }
   __shared__ double sL[BW * SS], sX[BW * SS];
-  load_tile(sL, Li, BW, BW, BW, t);
-  if (J < k)  // row block P of the lower storage
-    load_tile(sX, X + (size_t)(BW * k) * p + BW * J, p, wP, wJ, t);
-  else        // tile (J, k): X_{P,J}[r][c] = X[J*64 + c][k*64 + r]
-    load_tile_t(sX, X + (size_t)(BW * J) * p + BW * k, p, wP, wJ, t);
-  __syncthreads();
   const int wr = wv >> 1, wc = wv & 1;
   d4 acc[2][2];
 #pragma unroll
   for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
     for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4{0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < wP; k0 += 32)
+  for (int kh = 0; kh <= rh; ++kh) {
+    const int wk = min(BW, w - BW * kh);
+    const int I = P0 + kh;
+    if (kh) __syncthreads();
+    load_tile(sL, Li + (size_t)(BW * rh) * ldl + BW * kh, ldl, BW, BW, t);
+    if (J < P0)  // row block I of the lower storage
+      load_tile(sX, X + (size_t)(BW * I) * p + BW * J, p, wk, wJ, t);
+    else         // tile (J, I): X_{I,J}[r][c] = X[J*64 + c][I*64 + r]
+      load_tile_t(sX, X + (size_t)(BW * J) * p + BW * I, p, wk, wJ, t);
+    __syncthreads();
+    for (int k0 = 0; k0 < wk; k0 += 32)
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+      for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-        acc[bi][bj] = mma16(sL + k0, SS, 1, sX + k0 * SS, SS, 1, 32 * wr + 16 * bi, 32 * wc + 16 * bj,
-                            lane, acc[bi][bj]);
+        for (int bj = 0; bj < 2; ++bj)
+          acc[bi][bj] = mma16(sL + k0, SS, 1, sX + k0 * SS, SS, 1, 32 * wr + 16 * bi, 32 * wc + 16 * bj,
+                              lane, acc[bi][bj]);
+  }
 #pragma unroll
   for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -232,7 +368,7 @@ __global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 32 * wr + 16 * bi + (lane >> 4) + 4 * r, col = 32 * wc + 16 * bj + (lane & 15);
-        if (row < wP && col < wJ) Z[(size_t)row * p + BW * J + col] = acc[bi][bj][r];
+        if (row < hr && col < wJ) Z[(size_t)(BW * rh + row) * p + BW * J + col] = acc[bi][bj][r];
       }
 }
 
@@ -244,98 +380,125 @@ __device__ __forceinline__ void tile_of(int lin, int& I, int& J) {
   J = lin - i * (i + 1) / 2;
 }
 
-constexpr int UPD_WGS = 255;  // tile workgroups per factor (+1 pivot workgroup = one per CU)
-constexpr int SZ = 80;        // LDS stride of the Z panels [k][i]: k and k+1 32 banks apart
-
-// The tile list of one update launch: position 0 = (k+1,k+1) when there is a next pivot (so its
-// hand-off happens first), then every other lower tile in row-major order.
+// The tile list of one update launch: the nh tiles of the next pivot block (hand-off tiles) sit
+// at the first position of the runs of workgroups 0, 1, 2 (done first, by different workgroups),
+// every other lower tile follows in row-major order.
 struct TileList {
-  int k, ntiles, dk;
-  bool has_next;
+  int nt, nh;
+  int hlin[3];  // hand-off tiles' row-major lower indices, ascending
+  int hpos[3];  // their positions in the list
   __device__ void at(int pos, int& I, int& J) const {
-    if (has_next) {
-      if (pos == 0) { I = J = k + 1; return; }
-      int lin = pos - 1;
-      if (lin >= dk) ++lin;
-      tile_of(lin, I, J);
-    } else {
-      tile_of(pos, I, J);
-    }
+    for (int h = 0; h < nh; ++h)
+      if (pos == hpos[h]) {
+        tile_of(hlin[h], I, J);
+        return;
+      }
+    int lin = pos;
+    for (int h = 0; h < nh; ++h)
+      if (hpos[h] < pos) --lin;
+    for (int h = 0; h < nh; ++h)
+      if (lin >= hlin[h]) ++lin;
+    tile_of(lin, I, J);
+  }
+  __device__ bool handoff(int pos) const {
+    for (int h = 0; h < nh; ++h)
+      if (pos == hpos[h]) return true;
+    return false;
   }
 };
 
-// 64 x 64 panel block Z[0..63][c0..c0+63] -> registers (16 per thread, coalesced rows)
-__device__ __forceinline__ void zblock_fetch(double (&v)[16], const double* Z, int p, int c0, int wK, int t) {
+// Z panel block in LDS: 64 rows (k) x 64 columns (i), XOR-swizzled instead of padded: element
+// (k, i) at k*64 + (i ^ 16(k&1)) -- rows k and k+1 are 32 banks apart for the MFMA fragment
+// reads, as with a stride-80 layout, in 32 KB instead of 40
+__device__ __forceinline__ int zsw(int k, int i) { return k * 64 + (i ^ ((k & 1) << 4)); }
+
+// 64 x 64 panel block Z[rb..rb+63][c0..c0+63] -> registers (16 per thread, coalesced rows)
+__device__ __forceinline__ void zblock_fetch(double (&v)[16], const double* Z, int p, int rb, int c0, int wK,
+                                             int t) {
   const int c = t & 63, r0 = t >> 6;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    const int r = r0 + 4 * q;
+    const int r = rb + r0 + 4 * q;
     v[q] = (r < wK && c0 + c < p) ? Z[(size_t)r * p + c0 + c] : 0.0;
   }
 }
 __device__ __forceinline__ void zblock_store(const double (&v)[16], double* sZ, int t) {
   const int c = t & 63, r0 = t >> 6;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) sZ[(r0 + 4 * q) * SZ + c] = v[q];
+  for (int q = 0; q < 16; ++q) sZ[zsw(r0 + 4 * q, c)] = v[q];
 }
 
-constexpr int UPD_LDS = 2 * 64 * SZ + 64 * SS;  // sZI, sZJ, mirror stage (doubles)
+constexpr int UPD_LDS = 2 * 64 * 64;  // sZI, sZJ (doubles); the last sweep's mirror stage reuses them
 constexpr int BIG_LDS = UPD_LDS > PIVOT_LDS ? UPD_LDS : PIVOT_LDS;
 
-// One sweep's update of every lower tile (+ the next pivot, + the final sign flip / mirror).
-// Persistent: G <= 255 tile workgroups each take a contiguous run of the tile list (runs stay
-// within a block row, so Z_I is staged once per row); Z_I and Z_J sit in LDS, the next tile's
-// Z_J (and Z_I on a row change) is fetched into registers while the current tile's MFMAs run.
-// blockIdx.x: 0 = tile workgroup 0 (takes (k+1,k+1) first), 1 = the pivot workgroup,
-// 2.. = tile workgroups 1..  The pivot workgroup only waits for workgroup 0, dispatched
-// before it (resident or finished: no deadlock).
-__global__ __launch_bounds__(256) void big_update_kernel(BigSpdBatch b, int k, int skip_pivot) {
+// One sweep's update of every lower tile (+ the next pivot block, + the final sign flip / mirror).
+// Persistent: G tile workgroups per factor each take a contiguous run of the tile list; a tile
+// is R units (one per 64 rows of the panel): Z_I and Z_J of the unit sit in LDS, the next unit's
+// (and the next tile's X values) are fetched into registers while the current unit's MFMAs run.
+// At R = 1 a run stays within a block row mostly and Z_I is staged once per row.
+// blockIdx.x: 0 = tile workgroup 0, 1 = the pivot workgroup, 2.. = tile workgroups 1..  The pivot
+// workgroup waits for the hand-off tiles only; their workgroups never wait (no deadlock whatever
+// the residency).  LDS 67 KB and <= 256 VGPRs: two workgroups per CU.
+template <int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void big_update_kernel(BigSpdBatch b, int k, int skip_pivot) {
   const int m = blockIdx.y;
   const int p = b.p[m], T = b.T[m];
-  if (k >= T) return;
+  const int P0 = R * k;
+  if (P0 >= T) return;
+  const int nsw = (T + R - 1) / R;
+  const bool has_next = k + 1 < nsw;
+  const bool last = !has_next;
   TileList tl;
-  tl.k = k;
-  tl.ntiles = T * (T + 1) / 2;
-  tl.has_next = k + 1 < T;
-  tl.dk = (k + 1) * (k + 2) / 2 + (k + 1);
-  const bool last = !tl.has_next;
-  const int G = min(tl.ntiles, UPD_WGS);
+  tl.nt = T * (T + 1) / 2;
+  const int G = min(tl.nt, b.G);
+  const int chunk = (tl.nt + G - 1) / G;
+  tl.nh = 0;
+  if (has_next) {
+    const int Q0 = R * (k + 1);
+    tl.hlin[tl.nh++] = Q0 * (Q0 + 1) / 2 + Q0;
+    if (R == 2 && Q0 + 1 < T) {
+      tl.hlin[tl.nh++] = (Q0 + 1) * (Q0 + 2) / 2 + Q0;
+      tl.hlin[tl.nh++] = (Q0 + 1) * (Q0 + 2) / 2 + Q0 + 1;
+    }
+    for (int h = 0; h < tl.nh; ++h) tl.hpos[h] = h * chunk;
+  }
   const int x = blockIdx.x;
   __shared__ double sm[BIG_LDS];
   if (x == 1) {
-    if (!tl.has_next || skip_pivot) return;
+    if (!has_next || skip_pivot) return;
     if (threadIdx.x == 0) {  // pivot workgroup for block k+1
-      while (__hip_atomic_load(b.flag[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 1u)
+      while (__hip_atomic_load(b.flag[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)tl.nh)
         __builtin_amdgcn_s_sleep(2);
       *b.flag[m] = 0u;  // re-arm (next user: the next sweep's update launch)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    pivot64(b.X[m], p, k + 1, b.Li[m], b.ldet[m], b.status[m], sm);
+    pivot_block<R>(b, m, k + 1, sm);
     return;
   }
   const int g = x == 0 ? 0 : x - 1;
   if (g >= G) return;
-  const int chunk = (tl.ntiles + G - 1) / G;
-  const int pos0 = g * chunk, pos1 = min(tl.ntiles, pos0 + chunk);
+  const int pos0 = g * chunk, pos1 = min(tl.nt, pos0 + chunk);
   if (pos0 >= pos1) return;
   double* X = b.X[m];
   const double* Z = b.Z[m];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int li = lane & 15, lk = lane >> 4;
-  const int wK = bw(p, k);
+  const int wK = min(BW * R, p - BW * P0);  // sweep width
+  const int nhalf = (wK + BW - 1) / BW;     // units per tile (<= R)
   double* sZI = sm;
-  double* sZJ = sm + 64 * SZ;
-  double* sT = sm + 2 * 64 * SZ;  // [64][SS] transpose stage for the final mirror
+  double* sZJ = sm + 64 * 64;
+  double* sT = sm;  // [64][SS] transpose stage of the last sweep's mirror (after a barrier)
   const double fin = last ? -1.0 : 1.0;
+  auto inP = [&](int I_) { return I_ >= P0 && I_ < P0 + R; };
 
-  // X tile (I, J) in this wave's MFMA layout; zero base for the swept row / column block.
+  // X tile (I, J) in this wave's MFMA layout; zero base for the swept row / column blocks.
   // Unconditional clamped loads times a 0/1 factor (a guarded load would become an exec-mask
   // branch); rows / columns past p are never stored.
   auto xo_fetch = [&](double (&xv)[2][2][4], int I_, int J_) {
-    const double f = (I_ == k || J_ == k) ? 0.0 : 1.0;
+    const double f = (inP(I_) || inP(J_)) ? 0.0 : 1.0;
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -347,51 +510,58 @@ __global__ __launch_bounds__(256) void big_update_kernel(BigSpdBatch b, int k, i
           xv[bi][bj][r] = X[(size_t)gi * p + gj] * f;
         }
   };
-  int I, J;
+  int I, J, h = 0, pos = pos0;
   tl.at(pos0, I, J);
   double xo[2][2][4], xn[2][2][4];
   xo_fetch(xn, I, J);
   {
     double v[16];
-    zblock_fetch(v, Z, p, BW * I, wK, t);
+    zblock_fetch(v, Z, p, 0, BW * I, wK, t);
     zblock_store(v, sZI, t);
-    zblock_fetch(v, Z, p, BW * J, wK, t);
+    zblock_fetch(v, Z, p, 0, BW * J, wK, t);
     zblock_store(v, sZJ, t);
   }
   __syncthreads();
-  for (int pos = pos0; pos < pos1; ++pos) {
-    const int I0 = BW * I, J0 = BW * J;
-    const bool inPi = I == k, inPj = J == k;
+  d4 acc[2][2];
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+  for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
+    for (int bj = 0; bj < 2; ++bj) {
+      acc[bi][bj] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xo[bi][bj][r] = xn[bi][bj][r];
-    // the next tile's panels and X tile in flight under this tile's MFMAs
-    const bool more = pos + 1 < pos1;
-    int In = I, Jn = J;
-    double vj[16], vi[16];
-    if (more) {
-      tl.at(pos + 1, In, Jn);
-      zblock_fetch(vj, Z, p, BW * Jn, wK, t);
-      if (In != I) zblock_fetch(vi, Z, p, BW * In, wK, t);
-      xo_fetch(xn, In, Jn);
+      for (int r = 0; r < 4; ++r) xo[bi][bj][r] = xn[bi][bj][r];
     }
-    d4 acc[2][2];
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4{0.0, 0.0, 0.0, 0.0};
-    for (int k0 = 0; k0 < wK; k0 += 32) {
+  for (;;) {
+    // the next unit: its panel blocks (and, on a tile change, its X values) in flight under
+    // this unit's MFMAs
+    int hn = h + 1, posn = pos, In = I, Jn = J;
+    if (hn >= nhalf) {
+      hn = 0;
+      posn = pos + 1;
+    }
+    const bool more = posn < pos1;
+    const bool newtile = hn == 0;
+    double vj[16], vi[16];
+    bool ldI = false;
+    if (more) {
+      if (newtile) tl.at(posn, In, Jn);
+      // Z_I stays staged along a block row (R = 1), except in the last sweep, whose mirror
+      // stage overwrites it
+      ldI = R > 1 || In != I || last;
+      zblock_fetch(vj, Z, p, BW * hn, BW * Jn, wK, t);
+      if (ldI) zblock_fetch(vi, Z, p, BW * hn, BW * In, wK, t);
+      if (newtile) xo_fetch(xn, In, Jn);
+    }
+    const int kw = min(BW, wK - BW * h);
+    for (int k0 = 0; k0 < kw; k0 += 32) {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
-        const int kr = (k0 + 4 * kk + lk) * SZ;
+        const int kr = k0 + 4 * kk + lk;
         double a[2], bb[2];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          a[h] = sZI[kr + 32 * wr + 16 * h + li];
-          bb[h] = sZJ[kr + 32 * wc + 16 * h + li];
+        for (int q = 0; q < 2; ++q) {
+          a[q] = sZI[zsw(kr, 32 * wr + 16 * q + li)];
+          bb[q] = sZJ[zsw(kr, 32 * wc + 16 * q + li)];
         }
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
@@ -400,89 +570,129 @@ __global__ __launch_bounds__(256) void big_update_kernel(BigSpdBatch b, int k, i
             acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[bi], bb[bj], acc[bi][bj], 0, 0, 0);
       }
     }
-    const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * fin;
-    // tile (k+1,k+1) goes to the pivot workgroup: stored write-through (sc1), so the hand-off
-    // needs no L2 write-back (release fence) -- drain, barrier, one flag add (MI355X_MICROARCH
-    // §inter-workgroup visibility, "publish-large")
-    const bool handoff = tl.has_next && pos == 0;
-    double mx = 0.0;
+    if (h == nhalf - 1) {  // the tile is complete: epilogue
+      const int I0 = BW * I, J0 = BW * J;
+      const bool inPi = inP(I), inPj = inP(J);
+      const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * fin;
+      // the next pivot block's tiles go to the pivot workgroup: stored write-through (sc1), so
+      // the hand-off needs no L2 write-back (release fence) -- drain, barrier, one counter add
+      // (MI355X_MICROARCH §inter-workgroup visibility, "publish-large")
+      const bool handoff = has_next && tl.handoff(pos);
+      double mx = 0.0;
+      double vals[2][2][4];
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+      for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
+        for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 32 * wr + 16 * bi + lk + 4 * r, col = 32 * wc + 16 * bj + li;
-          const int gi = I0 + row, gj = J0 + col;
-          const double v = sgn * (xo[bi][bj][r] - acc[bi][bj][r]);
-          if (gi < p && gj < p) {
-            if (handoff)
-              __hip_atomic_store(&X[(size_t)gi * p + gj], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-              X[(size_t)gi * p + gj] = v;
-            if (last && I == J && gi == gj && gi < b.n[m]) mx = fmax(mx, v);
+          for (int r = 0; r < 4; ++r) {
+            const int row = 32 * wr + 16 * bi + lk + 4 * r, col = 32 * wc + 16 * bj + li;
+            const int gi = I0 + row, gj = J0 + col;
+            const double v = sgn * (xo[bi][bj][r] - acc[bi][bj][r]);
+            vals[bi][bj][r] = v;
+            if (gi < p && gj < p) {
+              if (handoff)
+                __hip_atomic_store(&X[(size_t)gi * p + gj], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              else
+                X[(size_t)gi * p + gj] = v;
+              if (last && I == J && gi == gj && gi < b.n[m]) mx = fmax(mx, v);
+            }
           }
-          if (last && I != J) sT[row * SS + col] = v;
-        }
-    if (handoff) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t == 0) atomicAdd(b.flag[m], 1u);
-    }
-    if (last && I == J) {  // refinement gate: max_i (K^{-1})_ii
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-      if (lane == 0 && mx > 0.0)
-        atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
-                  (unsigned long long)__double_as_longlong(mx));
-    }
-    __syncthreads();  // every wave is done reading sZI / sZJ (and has staged sT)
-    if (last && I != J) {
-      // mirror: X[J0 + r][I0 + c] = tile[c][r], coalesced along c
-      const int wI = bw(p, I), wJ = bw(p, J);
-#pragma unroll 4
-      for (int e = t; e < BW * BW; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        if (r < wJ && c < wI) X[(size_t)(J0 + r) * p + I0 + c] = sT[c * SS + r];
+      if (handoff) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) atomicAdd(b.flag[m], 1u);
       }
+      if (last && I == J) {  // refinement gate: max_i (K^{-1})_ii
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+        if (lane == 0 && mx > 0.0)
+          atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
+                    (unsigned long long)__double_as_longlong(mx));
+      }
+      if (last && I != J) {
+        __syncthreads();  // every wave is done reading sZI / sZJ: sT reuses them
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              sT[(32 * wr + 16 * bi + lk + 4 * r) * SS + 32 * wc + 16 * bj + li] = vals[bi][bj][r];
+        __syncthreads();
+        // mirror: X[J0 + r][I0 + c] = tile[c][r], coalesced along c
+        const int wI = bw(p, I), wJ = bw(p, J);
+#pragma unroll 4
+        for (int e = t; e < BW * BW; e += 256) {
+          const int r = e >> 6, c = e & 63;
+          if (r < wJ && c < wI) X[(size_t)(J0 + r) * p + I0 + c] = sT[c * SS + r];
+        }
+      }
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4{0.0, 0.0, 0.0, 0.0};
     }
+    __syncthreads();  // every wave is done reading sZI / sZJ (and sT)
     if (!more) break;
     zblock_store(vj, sZJ, t);
-    if (In != I) zblock_store(vi, sZI, t);
+    if (ldI) zblock_store(vi, sZI, t);
+    if (newtile) {
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xo[bi][bj][r] = xn[bi][bj][r];
+    }
     I = In;
     J = Jn;
+    h = hn;
+    pos = posn;
     __syncthreads();
   }
 }
+
+int batch_R(const SpdArgs* a) { return a[0].wide ? 2 : 1; }
 
 BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   BigSpdBatch b{};
   Tmax = 0;
   tiles_max = 0;
+  // two update workgroups per CU (67 KB LDS): the whole grid is one round over 256 CUs
+  b.G = g_big_wgs.load() > 0 ? g_big_wgs.load() : 512 / nmat - 1;
   for (int m = 0; m < nmat; ++m) {
     b.X[m] = a[m].X; b.Z[m] = a[m].Y; b.Li[m] = a[m].piv;
     b.ldet[m] = a[m].ldet; b.pst[m] = a[m].pst; b.status[m] = a[m].status; b.flag[m] = a[m].flag;
     b.p[m] = a[m].p; b.n[m] = a[m].n; b.T[m] = (a[m].p + BW - 1) / BW;
     Tmax = std::max(Tmax, b.T[m]);
-    tiles_max = std::max(tiles_max, std::min(b.T[m] * (b.T[m] + 1) / 2, UPD_WGS) + 1);
+    tiles_max = std::max(tiles_max, std::min(b.T[m] * (b.T[m] + 1) / 2, b.G) + 1);
   }
   return b;
 }
 
+template <int R>
+void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int stage, hipStream_t s) {
+  if (stage < 0)
+    hipLaunchKernelGGL(big_pivot_init_kernel<R>, dim3(nmat), dim3(256), 0, s, b);
+  else if ((stage & 1) == 0)
+    hipLaunchKernelGGL(big_panel_kernel<R>, dim3(Tmax * R, nmat), dim3(256), 0, s, b, stage >> 1);
+  else
+    hipLaunchKernelGGL(big_update_kernel<R>, dim3(tiles, nmat), dim3(256), 0, s, b, stage >> 1, 0);
+}
+
 }  // namespace
 
-int spd_big_sweeps(int p) { return (p + BW - 1) / BW; }
+int spd_big_sweeps(int p, int wide) { return (p + BW * (wide ? 2 : 1) - 1) / (BW * (wide ? 2 : 1)); }
+
+size_t spd_big_piv_doubles(int p) { return std::max<size_t>((size_t)p * 32, 128 * 128 + 2 * 64 * 64); }
 
 // stage -1: pivot 0; stage 2k: panel k; stage 2k+1: update k (profiling / bench)
 hipError_t launch_spd_big_stage(SpdArgs* a, int nmat, int stage, hipStream_t s) {
   int Tmax, tiles;
   BigSpdBatch b = make_batch(a, nmat, Tmax, tiles);
-  if (stage < 0)
-    hipLaunchKernelGGL(big_pivot_init_kernel, dim3(nmat), dim3(256), 0, s, b);
-  else if ((stage & 1) == 0)
-    hipLaunchKernelGGL(big_panel_kernel, dim3(Tmax, nmat), dim3(256), 0, s, b, stage >> 1);
-  else
-    hipLaunchKernelGGL(big_update_kernel, dim3(tiles, nmat), dim3(256), 0, s, b, stage >> 1, 0);
+  if (batch_R(a) == 2) launch_stage_r<2>(b, nmat, Tmax, tiles, stage, s);
+  else launch_stage_r<1>(b, nmat, Tmax, tiles, stage, s);
   return hipGetLastError();
 }
 
@@ -490,7 +700,10 @@ hipError_t launch_spd_big_stage(SpdArgs* a, int nmat, int stage, hipStream_t s) 
 hipError_t launch_spd_big_tiles(SpdArgs* a, int nmat, int k, hipStream_t s) {
   int Tmax, tiles;
   BigSpdBatch b = make_batch(a, nmat, Tmax, tiles);
-  hipLaunchKernelGGL(big_update_kernel, dim3(tiles, nmat), dim3(256), 0, s, b, k, 1);
+  if (batch_R(a) == 2)
+    hipLaunchKernelGGL(big_update_kernel<2>, dim3(tiles, nmat), dim3(256), 0, s, b, k, 1);
+  else
+    hipLaunchKernelGGL(big_update_kernel<1>, dim3(tiles, nmat), dim3(256), 0, s, b, k, 1);
   return hipGetLastError();
 }
 
@@ -498,10 +711,11 @@ hipError_t launch_spd_inverse_big(SpdArgs* a, int nmat, double** final_out, hipS
   int Tmax, tiles;
   BigSpdBatch b = make_batch(a, nmat, Tmax, tiles);
   for (int m = 0; m < nmat; ++m) final_out[m] = a[m].X;
-  hipLaunchKernelGGL(big_pivot_init_kernel, dim3(nmat), dim3(256), 0, s, b);
-  for (int k = 0; k < Tmax; ++k) {
-    hipLaunchKernelGGL(big_panel_kernel, dim3(Tmax, nmat), dim3(256), 0, s, b, k);
-    hipLaunchKernelGGL(big_update_kernel, dim3(tiles, nmat), dim3(256), 0, s, b, k, 0);
+  const int R = batch_R(a);
+  const int nsw = (Tmax + R - 1) / R;
+  for (int st = -1; st < 2 * nsw; ++st) {
+    if (R == 2) launch_stage_r<2>(b, nmat, Tmax, tiles, st, s);
+    else launch_stage_r<1>(b, nmat, Tmax, tiles, st, s);
   }
   return hipGetLastError();
 }

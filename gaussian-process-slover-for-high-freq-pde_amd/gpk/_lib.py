@@ -21,8 +21,10 @@ GPK_FLAG_FAST_FIRST = 32
 GPK_FLAG_NO_DCLASS = 64
 GPK_FLAG_NO_CHAIN = 128
 GPK_FLAG_NO_CHAIN_AUG = 256
-GPK_INV_SWEEP, GPK_INV_CHAIN, GPK_INV_CHAIN_AUG, GPK_INV_BIG = range(4)
-INV_PATH_NAMES = {0: "sweep", 1: "chain", 2: "chain_aug", 3: "big"}
+GPK_FLAG_FORCE_WIDE_SPD = 512
+GPK_FLAG_FORCE_NARROW_SPD = 1024
+GPK_INV_SWEEP, GPK_INV_CHAIN, GPK_INV_CHAIN_AUG, GPK_INV_BIG, GPK_INV_BIG_WIDE = range(5)
+INV_PATH_NAMES = {0: "sweep", 1: "chain", 2: "chain_aug", 3: "big", 4: "big_wide"}
 KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}
 EQ_IDS = {"poisson": 0, "allencahn": 1, "advection": 2}
 
@@ -93,6 +95,7 @@ EXPORTS = {
     "gpk_shard_info": ([ctypes.c_void_p, _ip, _ip, _ip, _ip], ctypes.c_int),
     "gpk_inverse_path": ([ctypes.c_void_p, _ip], ctypes.c_int),
     "gpk_set_chain_capacity": ([ctypes.c_int32], ctypes.c_int),
+    "gpk_set_spd_big_workgroups": ([ctypes.c_int32], ctypes.c_int),
     "gpk_graph_mode": ([ctypes.c_void_p, _ip, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
     "gpk_distance_classes": ([_dp, ctypes.c_int32, _ip, _ip], ctypes.c_int),
     "gpk_class_count": ([ctypes.c_void_p, ctypes.c_int32, _ip], ctypes.c_int),

@@ -291,6 +291,12 @@ def set_chain_capacity(workgroups):
     check(_lib.load().gpk_set_chain_capacity(int(workgroups)))
 
 
+def set_spd_big_workgroups(workgroups):
+    """Tile workgroups per factor of the large-factor inverse's update launch (0: default, two
+    per CU).  Tests use a few to give each workgroup long runs of tiles at small sizes."""
+    check(_lib.load().gpk_set_spd_big_workgroups(int(workgroups)))
+
+
 def comm_unique_id():
     """128-byte RCCL id for gpk_create_sharded (rank 0 makes it, every rank uses the same)."""
     buf = (ctypes.c_uint8 * 128)()

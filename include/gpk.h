@@ -103,6 +103,10 @@ typedef struct gpk_problem {
  * columns of the sweep operator and ends with A = K1^{-1} U, Bt = U K2^{-1} and K^{-1} D^T,
  * which replace the step's first GEMM stage and fold the X1/X2 solves into the G_D stage. */
 #define GPK_FLAG_NO_CHAIN_AUG 256  /* the chain inverts K only */
+/* Large factors (the panel/update inverse): 128-wide sweeps from a padded size of 3072 (the update
+ * is MFMA-bound instead of bound by the matrix traffic), 64-wide below (shorter serial pivots). */
+#define GPK_FLAG_FORCE_WIDE_SPD 512   /* 128-wide sweeps at every size (with FORCE_BIG_SPD: tests) */
+#define GPK_FLAG_FORCE_NARROW_SPD 1024 /* 64-wide sweeps at every size */
 
 typedef struct gpk_handle gpk_handle;
 
@@ -137,13 +141,16 @@ int gpk_destroy(gpk_handle* h);
 /* SPD inverse path a handle's step uses (chosen at gpk_create from the factor sizes, the flags
  * and the device): 32-wide per-sweep launches, the persistent chain (K^{-1} only / augmented
  * with the first solves), or the large-factor path. */
-enum { GPK_INV_SWEEP = 0, GPK_INV_CHAIN = 1, GPK_INV_CHAIN_AUG = 2, GPK_INV_BIG = 3 };
+enum { GPK_INV_SWEEP = 0, GPK_INV_CHAIN = 1, GPK_INV_CHAIN_AUG = 2, GPK_INV_BIG = 3, GPK_INV_BIG_WIDE = 4 };
 int gpk_inverse_path(const gpk_handle* h, int32_t* path);
 /* The chain's workgroups wait on one another, so gpk_create uses it only when its grid fits the
  * device's co-resident capacity (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs).  This
  * overrides that capacity for handles created afterwards (workgroups > 0; 0 restores the device
  * query) -- tests use it to force the per-sweep fallback. */
 int gpk_set_chain_capacity(int32_t workgroups);
+/* Tile workgroups per factor of the large-factor inverse's update launch (0: the default, two per
+ * CU).  Applies to every later launch; tests use a few to give each workgroup long tile runs. */
+int gpk_set_spd_big_workgroups(int32_t workgroups);
 
 /* Graph selection state (see GPK_FLAG_NO_FAST_GRAPH): *fast = 1 if the next gpk_step uses the
  * fast graph, *rollbacks = batches rerun with the full graph so far.  Either pointer may be NULL. */

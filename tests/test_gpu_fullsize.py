@@ -51,7 +51,7 @@ def test_c5_full_size_loss_grad_vs_oracle():
     prob, params, _, _ = _config_problem("C5")
     s = make_solver("C5", seed=0)
     try:
-        assert s.inverse_path() == "big"
+        assert s.inverse_path() == "big_wide"
         assert np.array_equal(s.get_flat(), O.flatten_params(params))  # same inputs as the oracle
         loss, g = s.loss_grad()
     finally:

@@ -78,12 +78,14 @@ def oracle_err(prob, params):
     return lo, go, errs
 
 
-def _cmp_lossgrad(prob, params, Q, fs, tol=None, flags=0, extended=True):
+def _cmp_lossgrad(prob, params, Q, fs, tol=None, flags=0, extended=True, path=None):
     """GPU vs oracle within max(cond_tol, 4 x the oracle's own distance from exact arithmetic):
     at cond(K) ~ 1e5..1e7 the reference algorithm itself is only good to ~1e-9 (kernel-parameter
     gradients through the explicit K^{-1} of slogdet's backward rule)."""
     tol = cond_tol(prob, params) if tol is None else tol
     s = device_solver(prob, Q, fs, flags=flags)
+    if path is not None:
+        assert s.inverse_path() == path
     s.set_params(params)
     loss, g = s.loss_grad()
     if extended:
@@ -223,38 +225,66 @@ def test_big_gemm_adam_and_predict_match_small():
         assert rel(out[0][2], o[2]) < 1e-10
 
 
+@pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("dim,eq,kind,n1,n2", [(1, "poisson", "Matern52_Cos_1d", 200, 0),
                                                (1, "allencahn", "SE_1d", 40, 0),
+                                               (1, "poisson", "SE_Cos_1d", 330, 0),
                                                (2, "poisson", "Matern52_Cos_1d", 96, 80),
                                                (2, "advection", "SE_Cos_1d", 72, 150),
                                                (2, "allencahn", "Matern52_1d", 130, 64)])
-def test_loss_grad_big_spd_path(dim, eq, kind, n1, n2):
-    """The 64-wide panel/update SPD inverse (spdinv_big.hip, used from p >= 768: C2, C5),
-    forced at small sizes: one-sweep factors (p=64), ragged last pivots of 32 (p=96, 160, 224),
-    in-launch pivot hand-off over several sweeps, the final mirror and the refinement gate."""
-    from gpk._lib import GPK_FLAG_FORCE_BIG_SPD
+def test_loss_grad_big_spd_path(dim, eq, kind, n1, n2, wide):
+    """The panel/update SPD inverse (spdinv_big.hip, used from p >= 1600: C2, C5), 64-wide and
+    128-wide sweeps, forced at small sizes: one-sweep factors (p=64, 96), ragged last pivots
+    of 32/64/96 (p=96, 160, 224, 352), the 128-pivot with a 32- or 64-wide second half, a last
+    sweep narrower than 64, in-launch pivot hand-off (1 or 3 tiles) over several sweeps, the
+    final mirror and the refinement gate."""
+    from gpk._lib import GPK_FLAG_FORCE_BIG_SPD, GPK_FLAG_FORCE_WIDE_SPD, GPK_FLAG_FORCE_NARROW_SPD
+    flags = GPK_FLAG_FORCE_BIG_SPD | (GPK_FLAG_FORCE_WIDE_SPD if wide else GPK_FLAG_FORCE_NARROW_SPD)
     if dim == 1:
         prob, params, _ = problem_1d(eq=eq, kind=kind, n=n1, Q=6, seed=3)
-        _cmp_lossgrad(prob, params, 6, 20.0, flags=GPK_FLAG_FORCE_BIG_SPD)
+        _cmp_lossgrad(prob, params, 6, 20.0, flags=flags, path="big_wide" if wide else "big")
     else:
         prob, params, _, fs = problem_2d(eq=eq, kind=kind, n1=n1, n2=n2, Q=5, seed=8)
-        _cmp_lossgrad(prob, params, 5, fs, flags=GPK_FLAG_FORCE_BIG_SPD)
+        _cmp_lossgrad(prob, params, 5, fs, flags=flags, path="big_wide" if wide else "big")
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_big_spd_long_tile_runs(wide):
+    """The update launch with 3 tile workgroups per factor: every workgroup walks a run of
+    tiles across block rows (panel blocks staged per unit and reused along a row at 64-wide,
+    the next unit prefetched under the current one's MFMAs, hand-off tiles at the start of
+    three runs, the last sweep's mirror stage reusing the panel LDS)."""
+    from gpk._lib import GPK_FLAG_FORCE_BIG_SPD, GPK_FLAG_FORCE_WIDE_SPD, GPK_FLAG_FORCE_NARROW_SPD
+    from gpk.core import set_spd_big_workgroups
+    flags = GPK_FLAG_FORCE_BIG_SPD | (GPK_FLAG_FORCE_WIDE_SPD if wide else GPK_FLAG_FORCE_NARROW_SPD)
+    set_spd_big_workgroups(3)
+    try:
+        prob, params, _ = problem_1d(eq="poisson", kind="Matern52_Cos_1d", n=330, Q=6, seed=4)
+        _cmp_lossgrad(prob, params, 6, 20.0, flags=flags)
+        prob, params, _, fs = problem_2d(eq="advection", kind="SE_Cos_1d", n1=200, n2=150, Q=5, seed=9)
+        _cmp_lossgrad(prob, params, 5, fs, flags=flags)
+    finally:
+        set_spd_big_workgroups(0)
 
 
 def test_big_spd_adam_and_predict_match_small():
-    """Same Adam trajectory and predictions with the large- and small-factor SPD inverses."""
-    from gpk._lib import GPK_FLAG_FORCE_BIG_SPD, GPK_FLAG_FORCE_SMALL_SPD
+    """Same Adam trajectory and predictions with the large- (64- and 128-wide sweeps) and the
+    small-factor SPD inverses."""
+    from gpk._lib import (GPK_FLAG_FORCE_BIG_SPD, GPK_FLAG_FORCE_SMALL_SPD, GPK_FLAG_FORCE_WIDE_SPD,
+                          GPK_FLAG_FORCE_NARROW_SPD)
     prob, params, (Xte, _), fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=200, n2=136, Q=6, seed=2)
     out = []
-    for flags in (GPK_FLAG_FORCE_SMALL_SPD, GPK_FLAG_FORCE_BIG_SPD):
+    for flags in (GPK_FLAG_FORCE_SMALL_SPD, GPK_FLAG_FORCE_BIG_SPD | GPK_FLAG_FORCE_NARROW_SPD,
+                  GPK_FLAG_FORCE_BIG_SPD | GPK_FLAG_FORCE_WIDE_SPD):
         s = device_solver(prob, 6, fs, flags=flags)
         s.set_params(params)
         losses = s.step(10)
         out.append((losses, s.get_flat(), s.predict(Xte[0], Xte[1])))
         s.close()
-    assert rel(out[0][0], out[1][0]) < 1e-10
-    assert rel(out[0][1], out[1][1]) < 1e-8
-    assert rel(out[0][2], out[1][2]) < 1e-9
+    for o in out[1:]:
+        assert rel(out[0][0], o[0]) < 1e-10
+        assert rel(out[0][1], o[1]) < 1e-8
+        assert rel(out[0][2], o[2]) < 1e-9
 
 
 def test_loss_grad_1d_c2_size():
