@@ -33,6 +33,7 @@
 // the 128-pivot is the same recursion one level up with 64-pivots and 64x64 products.
 #include <atomic>
 
+#include "gemm_huge_dev.h"
 #include "gpk_internal.h"
 #include "spd_pivot.h"
 
@@ -43,7 +44,6 @@ void spd_big_set_workgroups(int g) { g_big_wgs.store(g > 0 ? g : 0); }
 
 namespace {
 
-typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int BW = 64;   // tile width (and the 64-pivot)
 constexpr int SS = 65;   // 64x64 LDS tile stride (doubles)
 
@@ -653,14 +653,133 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
+// ---- 128-wide sweeps: the update on 128x128 tiles (the large GEMM's tile loop) ------------
+// One workgroup per LOWER 128x128 tile (ti >= tj) computes Z_I^T Z_J with gemm_huge_dev.h's
+// product loop (K = the sweep width, 16-deep double-buffered LDS steps, 4x4 MFMA blocks per wave)
+// and applies the sweep's epilogue (sign, zero base in the swept row / column).  Diagonal tiles
+// keep both triangles of their 128 block, so every lower 64-tile the panel reads is current.
+// Workgroup 0 of a factor owns the next pivot block's tile (k+1, k+1): it updates it like the
+// others, then factors it in place (pivot128: Cholesky + L^{-1}) while the other tiles are
+// updated -- no hand-off, no workgroup waits on another.  The last sweep flips the sign and
+// publishes max diag K^{-1}; big_mirror_kernel then fills the upper triangle.
+constexpr int WT = 128;
+constexpr int WIDE_LDS = 2 * 2 * huge::KS * huge::S;  // the product loop's two staging buffers
+static_assert(WIDE_LDS >= PIVOT_LDS, "the pivot reuses the staging LDS");
+
+__global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, int skip_pivot) {
+  using namespace huge;
+  const int m = blockIdx.y;
+  const int p = b.p[m];
+  const int T2 = (p + WT - 1) / WT;  // 128-tiles per dimension
+  if (k >= T2) return;
+  const bool has_next = k + 1 < T2;
+  const bool LAST = !has_next;  // (per factor: the factors of a batch may differ in size)
+  const int nt = T2 * (T2 + 1) / 2;
+  const int Q = k + 1, qlin = Q * (Q + 1) / 2 + Q;
+  const int x = blockIdx.x;
+  int ti, tj;
+  const bool pivot = x == 0;
+  if (pivot) {
+    if (!has_next || skip_pivot) return;
+    ti = tj = Q;
+  } else {
+    int lin = x - 1;
+    if (lin >= nt - (has_next ? 1 : 0)) return;
+    if (has_next && lin >= qlin) ++lin;  // (k+1, k+1) belongs to the pivot workgroup
+    tile_of(lin, ti, tj);
+  }
+  __shared__ double sm[WIDE_LDS];
+  double* X = b.X[m];
+  const double* Z = b.Z[m];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int i0 = WT * ti, j0 = WT * tj;
+  const int wK = min(WT, p - WT * k);  // sweep width (a multiple of 32)
+  const bool inPi = ti == k, inPj = tj == k;
+  const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
+  // the tile's current values, in flight under the product (zero base in the swept blocks;
+  // clamped addresses: rows / columns past p are never stored).  Held in registers: one wave
+  // per SIMD (measured: 4.97 ms for C5's two 4096 factors, against 5.34 ms at two waves per
+  // SIMD with the base loaded in the epilogue)
+  double xb[4][4][4];
+  const double f = (inPi || inPj) ? 0.0 : 1.0;
+#pragma unroll
+  for (int bx = 0; bx < 4; ++bx)
+#pragma unroll
+    for (int by = 0; by < 4; ++by)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = min(i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r, p - 1);
+        const int col = min(j0 + 64 * wc + 16 * by + (lane & 15), p - 1);
+        xb[bx][by][r] = X[(size_t)row * p + col] * f;
+      }
+  d4 acc[4][4];
+#pragma unroll
+  for (int bx = 0; bx < 4; ++bx)
+#pragma unroll
+    for (int by = 0; by < 4; ++by) acc[bx][by] = d4{0.0, 0.0, 0.0, 0.0};
+  // Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j])
+  product_t<1, 0>(Z, p, Z, p, wK, p, p, i0, j0, 1.0, sm, sm + 2 * KS * S, t, wr, wc, lane, acc);
+  double mx = 0.0;
+#pragma unroll
+  for (int bx = 0; bx < 4; ++bx) {
+#pragma unroll
+    for (int by = 0; by < 4; ++by)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r;
+        const int col = j0 + 64 * wc + 16 * by + (lane & 15);
+        if (row < p && col < p) {
+          const double v = sgn * (xb[bx][by][r] - acc[bx][by][r]);
+          X[(size_t)row * p + col] = v;
+          if (LAST && row == col && row < b.n[m]) mx = fmax(mx, v);
+        }
+      }
+    asm volatile("" ::: "memory");
+  }
+  if (LAST && ti == tj) {  // refinement gate: max_i (K^{-1})_ii
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0 && mx > 0.0)
+      atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
+                (unsigned long long)__double_as_longlong(mx));
+  }
+  if (!pivot) return;
+  // the next pivot block, factored in place from this workgroup's own stores (one L1 per
+  // workgroup: visible after the barrier)
+  __syncthreads();
+  const int r0 = WT * Q, w = min(WT, p - r0);
+  pivot128(X + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 4 * Q, b.status[m], sm);
+}
+
+// After the last 128-wide sweep: upper 64x64 tiles outside the diagonal 128 blocks <- the
+// transposed lower ones (LDS transpose, coalesced loads and stores).
+__global__ __launch_bounds__(256) void big_mirror_kernel(BigSpdBatch b) {
+  const int m = blockIdx.y;
+  const int p = b.p[m], T = b.T[m];
+  int I, J;
+  tile_of(blockIdx.x, I, J);
+  if (I >= T || I == J || (I >> 1) == (J >> 1)) return;
+  __shared__ double sT[BW * SS];
+  double* X = b.X[m];
+  const int wI = bw(p, I), wJ = bw(p, J);
+  load_tile(sT, X + (size_t)(BW * I) * p + BW * J, p, wI, wJ, threadIdx.x);
+  __syncthreads();
+  for (int e = threadIdx.x; e < BW * BW; e += 256) {
+    const int r = e >> 6, c = e & 63;  // X[J*64 + r][I*64 + c] = tile[c][r]
+    if (r < wJ && c < wI) X[(size_t)(BW * J + r) * p + BW * I + c] = sT[c * SS + r];
+  }
+}
+
 int batch_R(const SpdArgs* a) { return a[0].wide ? 2 : 1; }
 
 BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   BigSpdBatch b{};
   Tmax = 0;
   tiles_max = 0;
-  // two update workgroups per CU (67 KB LDS): the whole grid is one round over 256 CUs
-  b.G = g_big_wgs.load() > 0 ? g_big_wgs.load() : 512 / nmat - 1;
+  // 64-wide update: 255 tile workgroups per factor (+ its pivot workgroup; two fit per CU).
+  // Measured at 2048: 1177 us per inverse vs 1243 us with 383 or 511
+  b.G = g_big_wgs.load() > 0 ? g_big_wgs.load() : 255;
   for (int m = 0; m < nmat; ++m) {
     b.X[m] = a[m].X; b.Z[m] = a[m].Y; b.Li[m] = a[m].piv;
     b.ldet[m] = a[m].ldet; b.pst[m] = a[m].pst; b.status[m] = a[m].status; b.flag[m] = a[m].flag;
@@ -671,14 +790,29 @@ BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   return b;
 }
 
+// workgroups of one 128-wide update launch: the pivot workgroup + one per lower 128-tile
+int wide_tiles(int Tmax) {
+  const int T2 = (Tmax + 1) / 2;
+  return 1 + T2 * (T2 + 1) / 2;
+}
+
 template <int R>
-void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int stage, hipStream_t s) {
-  if (stage < 0)
+void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int stage, hipStream_t s,
+                    int skip_pivot = 0) {
+  if (stage < 0) {
     hipLaunchKernelGGL(big_pivot_init_kernel<R>, dim3(nmat), dim3(256), 0, s, b);
-  else if ((stage & 1) == 0)
+  } else if ((stage & 1) == 0) {
     hipLaunchKernelGGL(big_panel_kernel<R>, dim3(Tmax * R, nmat), dim3(256), 0, s, b, stage >> 1);
-  else
-    hipLaunchKernelGGL(big_update_kernel<R>, dim3(tiles, nmat), dim3(256), 0, s, b, stage >> 1, 0);
+  } else if (R == 1) {
+    hipLaunchKernelGGL(big_update_kernel<1>, dim3(tiles, nmat), dim3(256), 0, s, b, stage >> 1, skip_pivot);
+  } else {
+    const int k = stage >> 1, nsw = (Tmax + 1) / 2;
+    hipLaunchKernelGGL(wide_update_kernel, dim3(wide_tiles(Tmax), nmat), dim3(256), 0, s, b, k, skip_pivot);
+    // after the last sweep of every factor (a smaller factor's last sweep came earlier; later
+    // launches leave it alone)
+    if (k + 1 == nsw)
+      hipLaunchKernelGGL(big_mirror_kernel, dim3(Tmax * (Tmax + 1) / 2, nmat), dim3(256), 0, s, b);
+  }
 }
 
 }  // namespace
@@ -700,10 +834,8 @@ hipError_t launch_spd_big_stage(SpdArgs* a, int nmat, int stage, hipStream_t s) 
 hipError_t launch_spd_big_tiles(SpdArgs* a, int nmat, int k, hipStream_t s) {
   int Tmax, tiles;
   BigSpdBatch b = make_batch(a, nmat, Tmax, tiles);
-  if (batch_R(a) == 2)
-    hipLaunchKernelGGL(big_update_kernel<2>, dim3(tiles, nmat), dim3(256), 0, s, b, k, 1);
-  else
-    hipLaunchKernelGGL(big_update_kernel<1>, dim3(tiles, nmat), dim3(256), 0, s, b, k, 1);
+  if (batch_R(a) == 2) launch_stage_r<2>(b, nmat, Tmax, tiles, 2 * k + 1, s, 1);
+  else launch_stage_r<1>(b, nmat, Tmax, tiles, 2 * k + 1, s, 1);
   return hipGetLastError();
 }
 

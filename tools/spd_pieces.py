@@ -8,10 +8,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process-slover-for-high-freq-pde_amd")]
 from gpk import problems
 from gpk._lib import GPK_FLAG_FORCE_BIG_SPD, GPK_FLAG_FORCE_WIDE_SPD, GPK_FLAG_FORCE_NARROW_SPD
+from gpk.core import set_spd_big_workgroups
 
 sizes = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "256,1024,2048,4096").split(",")]
 which = sys.argv[2] if len(sys.argv) > 2 else "both"
 widths = {"narrow": [False], "wide": [True], "both": [False, True]}[which]
+set_spd_big_workgroups(int(sys.argv[3]) if len(sys.argv) > 3 else 0)  # 64-wide update workgroups
 for n in sizes:
     for wide in widths:
         flags = GPK_FLAG_FORCE_BIG_SPD | (GPK_FLAG_FORCE_WIDE_SPD if wide else GPK_FLAG_FORCE_NARROW_SPD)
