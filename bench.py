@@ -139,15 +139,19 @@ def large_factors(steps=3):
             "spd_update_tflops": tfl / (tus * 1e-6) / 1e12}
 
 
-def sharded_section(a, ctx, configs=("C4", "C5")):
+def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
     """ONE problem per config row-sharded over all ranks (gpk/shard.py: rows of every product
     per rank, RCCL all-gathers / all-reduces inside the step graph).  value = steps/s of the
-    single problem (strong scaling)."""
+    single problem (strong scaling).  C5_split: one Kronecker factor inverted per rank half,
+    broadcast over RCCL (GPK_FLAG_SPLIT_FACTORS) instead of both factors on every rank."""
     from gpk import replicas, shard
+    from gpk._lib import GPK_FLAG_SPLIT_FACTORS
     out = {}
-    for cid in configs:
+    for key in configs:
+        cid = key.split("_")[0]
+        flags = GPK_FLAG_SPLIT_FACTORS if key.endswith("_split") else 0
         steps = a.sharded_steps if cid == "C4" else max(2, a.sharded_steps // 10)
-        s = shard.make_sharded_solver(cid, ctx, seed=0)
+        s = shard.make_sharded_solver(cid, ctx, seed=0, flags=flags)
         try:
             s.prepare(steps)
             s.step(2)
@@ -159,7 +163,7 @@ def sharded_section(a, ctx, configs=("C4", "C5")):
         finally:
             s.close()
         dt = replicas.max_over_ranks(t1 - t0, ctx)
-        out[cid] = {"value": steps / dt, "unit": "iters/s", "ms_per_step": dt / steps * 1e3,
+        out[key] = {"value": steps / dt, "unit": "iters/s", "ms_per_step": dt / steps * 1e3,
                     "steps": steps, "ranks": ctx.world}
     return out
 

@@ -137,6 +137,7 @@ struct gpk_handle {
   // row-sharded step: this rank computes rows [rank*h, (rank+1)*h) of every GEMM output
   bool shard = false;
   int rank = 0, nranks = 1;
+  int split_axis = -1;                // GPK_FLAG_SPLIT_FACTORS: the factor this rank inverts
   int h1 = 0, h2 = 0;                 // row-block heights of the P1- and P2-row outputs
   ShardComm* comm = nullptr;
   std::vector<GemmDesc> sdescs;       // row slices of hdescs
@@ -267,6 +268,8 @@ static hipError_t launch_inverse(gpk_handle* h, SpdArgs* sa, double** fin, bool 
   return launch_spd_inverse(sa, h->L.naxes, fin, h->s, pivot0_done);
 }
 
+static int split_broadcast(gpk_handle* h);  // (after ShardComm)
+
 // assemble K, D (+ step constants, + pivot block 0) and invert K: the first part of a step
 static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
   const Layout& L = h->L;
@@ -302,10 +305,23 @@ static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
   SpdArgs sa[2];
   fill_spd(h, sa);
   double* fin[2] = {nullptr, nullptr};
-  if (h->chain)
+  if (h->chain) {
     TRY(check_launch(launch_chain(h, eval_only, fin, true, eval_only ? &prep : nullptr), "spd_chain"));
-  else
+  } else if (h->split_axis >= 0) {
+    // one factor per rank group: invert this rank's factor, then every factor's K^{-1}, log-det
+    // blocks and refinement gate from its group's first rank (the other factor's buffers on
+    // this rank are overwritten; the sweep path's output buffer is fixed per factor size)
+    const int a = h->split_axis;
+    double* f1[1] = {nullptr};
+    if (h->bigspd)
+      TRY(check_launch(launch_spd_inverse_big(sa + a, 1, f1, h->s), "spd_inverse"));
+    else
+      TRY(check_launch(launch_spd_inverse(sa + a, 1, f1, h->s, true), "spd_inverse"));
+    TRY(split_broadcast(h));
+    for (int b = 0; b < L.naxes; ++b) fin[b] = h->Kinv[b];
+  } else {
     TRY(check_launch(launch_inverse(h, sa, fin, true), "spd_inverse"));
+  }
   for (int a = 0; a < L.naxes; ++a) h->Kinv[a] = fin[a];
   mark(h, 2);
   return GPK_OK;
@@ -672,6 +688,7 @@ struct ShardComm {
   virtual ~ShardComm() {}
   virtual int allgather(gpk_handle* h, double* buf, size_t chunk) = 0;  // in place
   virtual int allreduce(gpk_handle* h, double* buf, size_t n) = 0;      // in place, sum
+  virtual int broadcast(gpk_handle* h, double* buf, size_t n, int root) = 0;  // in place
   virtual bool capturable() const = 0;
 };
 
@@ -689,6 +706,10 @@ struct RcclComm : ShardComm {
   int allreduce(gpk_handle* h, double* buf, size_t n) override {
     ncclResult_t r = ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c, h->s);
     return r == ncclSuccess ? GPK_OK : fail(GPK_ERCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  }
+  int broadcast(gpk_handle* h, double* buf, size_t n, int root) override {
+    ncclResult_t r = ncclBroadcast(buf, buf, n, ncclDouble, root, c, h->s);
+    return r == ncclSuccess ? GPK_OK : fail(GPK_ERCCL, std::string("ncclBroadcast: ") + ncclGetErrorString(r));
   }
   bool capturable() const override { return true; }
 };
@@ -758,6 +779,21 @@ struct LocalComm : ShardComm {
     if (!g->barrier()) return fail(GPK_EHIP, "rank group aborted");
     return rc;
   }
+  int broadcast(gpk_handle* h, double* buf, size_t n, int root) override {
+    HIPCHK(hipStreamSynchronize(h->s));
+    g->slot[h->rank] = buf;
+    if (!g->barrier()) return fail(GPK_EHIP, "rank group aborted");
+    int rc = GPK_OK;
+    if (h->rank == 0) {
+      for (int dst = 0; dst < g->n && rc == GPK_OK; ++dst)
+        if (dst != root && hipMemcpyAsync(g->slot[dst], g->slot[root], n * sizeof(double),
+                                          hipMemcpyDeviceToDevice, h->s) != hipSuccess)
+          rc = fail(GPK_EHIP, "group broadcast copy");
+      if (hipStreamSynchronize(h->s) != hipSuccess) rc = fail(GPK_EHIP, "group broadcast sync");
+    }
+    if (!g->barrier()) return fail(GPK_EHIP, "rank group aborted");
+    return rc;
+  }
   bool capturable() const override { return false; }
 };
 
@@ -789,7 +825,34 @@ GemmDesc slice_rows(const GemmDesc& d, int r0, int rows, int variant) {
   return s;
 }
 
+// rows [r0, r0 + rows) of the CONTRACTION index of C = op(A) op(B) (single product): this rank's
+// partial of a full-size C, summed over ranks only through the linear parameter contraction.
+// The C0 term is carried by rank 0 alone.
+GemmDesc slice_k(const GemmDesc& d, int r0, int rows, int rank) {
+  GemmDesc s = d;
+  s.K = rows;
+  s.A = d.ta ? d.A + (size_t)r0 * d.lda : d.A + r0;
+  s.B = d.tb ? d.B + r0 : d.B + (size_t)r0 * d.ldb;
+  if (rank != 0) {
+    s.C0 = nullptr;
+    s.beta = 0.0;
+  }
+  return s;
+}
+
 }  // namespace
+
+// GPK_FLAG_SPLIT_FACTORS: factor b's K^{-1}, log-det blocks and gate from its group's first rank
+static int split_broadcast(gpk_handle* h) {
+  const Layout& L = h->L;
+  for (int b = 0; b < 2; ++b) {
+    const int P = b == 0 ? L.p1 : L.p2, root = b == 0 ? 0 : h->nranks / 2;
+    TRY(h->comm->broadcast(h, h->Kinv[b], (size_t)P * P, root));
+    TRY(h->comm->broadcast(h, h->ldet[b], (size_t)P / 32, root));
+    TRY(h->comm->broadcast(h, h->pst[b], 2, root));
+  }
+  return GPK_OK;
+}
 
 // Row slices of the step's GEMM stages for this rank, the variant per stage (its tile rows must
 // divide the slice height so that the per-tile loss partials land in the full-grid slots), and
@@ -806,36 +869,48 @@ static int build_shard(gpk_handle* h) {
     const int n = h->st[k].n;
     std::vector<GemmDesc> tmp;
     auto rows_of = [&](const GemmDesc& d) { return d.M == P1 ? h->h1 : h->h2; };
+    // G_K2 = c N1/2 K2^{-1} - Y2^T Bt and G_D2 = v R^T Bt contract over the P1 rows: each rank
+    // forms the full matrix from its own rows of Y2 / R and Bt (no all-gather of those operands)
+    auto ksplit = [&](const GemmDesc& d) { return d.C == h->GK[1] || d.C == h->GD[1]; };
     for (int i = 0; i < n; ++i) {
       const GemmDesc& d = full[i];
       if (d.M != P1 && d.M != P2) return fail(GPK_EINVAL, "shard: unexpected GEMM row count");
       const int rows = rows_of(d);
-      tmp.push_back(slice_rows(d, h->rank * rows, rows, GEMM_SMALL));
+      tmp.push_back(ksplit(d) ? slice_k(d, h->rank * h->h1, h->h1, h->rank)
+                              : slice_rows(d, h->rank * rows, rows, GEMM_SMALL));
     }
     int variant = gemm_variant(tmp.data(), n, force);
     for (int i = 0; i < n; ++i)
-      while (rows_of(full[i]) % tile_rows(variant) != 0) variant = variant == GEMM_HUGE ? GEMM_BIG : GEMM_SMALL;
+      while (!ksplit(full[i]) && rows_of(full[i]) % tile_rows(variant) != 0)
+        variant = variant == GEMM_HUGE ? GEMM_BIG : GEMM_SMALL;
     h->sst[k].off = (int)h->sdescs.size();
     h->sst[k].n = n;
     h->sst[k].variant = variant;
     for (int i = 0; i < n; ++i) {
       const int rows = rows_of(full[i]);
-      h->sdescs.push_back(slice_rows(full[i], h->rank * rows, rows, variant));
+      h->sdescs.push_back(ksplit(full[i]) ? slice_k(full[i], h->rank * h->h1, h->h1, h->rank)
+                                          : slice_rows(full[i], h->rank * rows, rows, variant));
       if (full[i].red) h->nquad = h->negap = gemm_tiles(full[i], variant);
     }
   }
+  // All-gathers: exactly the operands a later product reads beyond this rank's rows.  G_K / G_D
+  // are never gathered: axis 1's are row slices (the other rows stay zero on this rank), axis
+  // 2's this rank's partials (slice_k); the parameter contraction is linear in them, so every
+  // rank contracts what it holds and the partials are all-reduced (enqueue_step_shard).
   auto g1 = [&](double* b) { return ShardGather{b, (size_t)h->h1 * P2}; };
   for (auto& v : h->sgather) v.clear();
-  h->sgather[0] = {g1(h->A)};                                  // A_res: K1 A
-  h->sgather[1] = {g1(h->W1)};                                 // A_fix: K1^{-1} W1
-  h->sgather[2] = {g1(h->A), g1(h->Bt)};                       // R: D1 A; G_D*, G_K*: A^T, Bt
-  h->sgather[3] = {g1(h->R)};                                  // T1 = D1^T R; G_D2 = R^T Bt
-  h->sgather[6] = {g1(h->T1), ShardGather{h->GD[0], (size_t)h->h1 * P1},  // X1 = K1^{-1} T1;
-                   ShardGather{h->GD[1], (size_t)h->h2 * P2}};            // pgrad reads G_D whole
-  h->sgather[7] = {g1(h->X1)};                                 // D_res: K1 X1
-  h->sgather[8] = {g1(h->W1)};                                 // D_fix: K1^{-1} W1
-  h->sgather[9] = {g1(h->Y2)};                                 // G_K2: Y2^T Bt (Y2 = S/2 + v X2)
-  h->sgather[10] = {ShardGather{h->GK[0], (size_t)h->h1 * P1}, ShardGather{h->GK[1], (size_t)h->h2 * P2}};
+  const bool refine = h->st[1].n > 0;  // (2D large factors: no refinement stages)
+  if (refine) {
+    h->sgather[0] = {g1(h->A)};                                // A_res: K1 A
+    h->sgather[1] = {g1(h->W1)};                               // A_fix: K1^{-1} W1
+  }
+  h->sgather[2] = {g1(h->A)};                                  // R: D1 A;  G_K1 = Y1 A^T
+  h->sgather[3] = {g1(h->R)};                                  // T1 = D1^T R
+  h->sgather[6] = {g1(h->T1)};                                 // X1 = K1^{-1} T1
+  if (refine) {
+    h->sgather[7] = {g1(h->X1)};                               // D_res: K1 X1
+    h->sgather[8] = {g1(h->W1)};                               // D_fix: K1^{-1} W1
+  }
   return GPK_OK;
 }
 
@@ -843,8 +918,9 @@ static int enqueue_step_shard(gpk_handle* h, int apply) {
   const Layout& L = h->L;
   TRY(enqueue_assemble_inverse(h, apply));  // replicated: K, D, K^{-1}, log det, step constants
   for (int k = 0; k < kGemmStages; ++k) {
-    TRY(check_launch(launch_gemm_auto(h->sdescs.data() + h->sst[k].off, h->sst[k].n, h->sc, h->s,
-                                      h->sst[k].variant), "gemm"));
+    if (h->sst[k].n)  // (empty: a refinement stage of a path without refinement)
+      TRY(check_launch(launch_gemm_auto(h->sdescs.data() + h->sst[k].off, h->sst[k].n, h->sc, h->s,
+                                        h->sst[k].variant), "gemm"));
     for (const ShardGather& g : h->sgather[k]) TRY(h->comm->allgather(h, g.buf, g.chunk));
   }
   PGradArgs pa[2];
@@ -860,8 +936,8 @@ static int enqueue_step_shard(gpk_handle* h, int apply) {
     pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
     pa[a].cls = h->cls[a];
   }
-  TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, nullptr, h->rank,
-                                h->nranks), "pgrad"));
+  // every rank contracts its own G_K / G_D rows (axis 1) and partials (axis 2) in full
+  TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, nullptr), "pgrad"));
   TRY(check_launch(launch_reduce_parts(h->pgpart, h->bpa, 2, L.q, h->pg, h->s), "reduce_parts"));
   TRY(h->comm->allreduce(h, h->pg, (size_t)2 * 3 * QMAX));
   TRY(h->comm->allreduce(h, h->red_egap, (size_t)h->negap));
@@ -1132,7 +1208,10 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
       return wide * L.naxes;
     };
     const bool in_group = shard && local_group && nranks > 1;
-    h->chain = !h->bigspd && !in_group && !(p->flags & GPK_FLAG_NO_CHAIN) && grid_blocks(false) <= cap;
+    if (shard && nranks >= 2 && (p->flags & GPK_FLAG_SPLIT_FACTORS)) h->split_axis = rank < nranks / 2 ? 0 : 1;
+    // (the chain inverts every factor in one launch: a split rank inverts one, per sweep)
+    h->chain = !h->bigspd && !in_group && h->split_axis < 0 && !(p->flags & GPK_FLAG_NO_CHAIN) &&
+               grid_blocks(false) <= cap;
     h->chain_aug = h->chain && L.dim == 2 && !shard && !(p->flags & GPK_FLAG_NO_CHAIN_AUG) &&
                    grid_blocks(true) <= cap;
   }

@@ -107,6 +107,10 @@ typedef struct gpk_problem {
  * is MFMA-bound instead of bound by the matrix traffic), 64-wide below (shorter serial pivots). */
 #define GPK_FLAG_FORCE_WIDE_SPD 512   /* 128-wide sweeps at every size (with FORCE_BIG_SPD: tests) */
 #define GPK_FLAG_FORCE_NARROW_SPD 1024 /* 64-wide sweeps at every size */
+/* Row-sharded handles (nranks >= 2): the first half of the ranks inverts K1 only, the second half
+ * K2 only, and the inverses (+ their log-det blocks and refinement gates) are broadcast from
+ * ranks 0 and nranks/2 -- one Kronecker factor per rank group instead of both on every rank. */
+#define GPK_FLAG_SPLIT_FACTORS 2048
 
 typedef struct gpk_handle gpk_handle;
 

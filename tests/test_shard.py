@@ -114,6 +114,66 @@ def test_group_trajectory_matches_unsharded(nranks, flags):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nranks,big", [(2, False), (3, False), (4, True), (5, True)])
+def test_group_split_factors_matches_unsharded(nranks, big):
+    """GPK_FLAG_SPLIT_FACTORS: ranks [0, n/2) invert K1 only, [n/2, n) K2 only, and the inverses,
+    log-det blocks and refinement gates are broadcast from ranks 0 and n/2.  Loss, gradient and
+    a 5-step Adam trajectory vs one unsharded handle, with the per-sweep and the large-factor
+    (forced, 64- and 128-wide) inverses; odd rank counts give unequal groups."""
+    from gpk._lib import (GPK_FLAG_SPLIT_FACTORS, GPK_FLAG_FORCE_BIG_SPD, GPK_FLAG_FORCE_WIDE_SPD,
+                          GPK_FLAG_NO_CHAIN)
+    prob, params, _, fs = problem_2d(eq="advection", kind="Matern52_Cos_1d", n1=150, n2=96, Q=5, seed=22)
+    extra = (GPK_FLAG_FORCE_BIG_SPD | (GPK_FLAG_FORCE_WIDE_SPD if nranks == 5 else 0)) if big else 0
+    g = _group(prob, 5, fs, nranks, flags=GPK_FLAG_SPLIT_FACTORS | extra)
+    s = device_solver(prob, 5, fs, flags=NO_AUG | GPK_FLAG_NO_CHAIN | extra)
+    try:
+        g.set_params(params)
+        s.set_params(params)
+        lg, gg = g.loss_grad()
+        ls, gs = s.loss_grad()
+        assert abs(lg - ls) / abs(ls) < 1e-11, (lg, ls)
+        assert rel(gg, gs) < 1e-9
+        lo, go = O.loss_grad_2d(prob, params)
+        assert rel(gg, O.flatten_params(go)) < _tol(prob, params)
+        # the row-sliced and K-split products sum in another order than one handle's; cond(K)
+        # lifts those rounding differences over the trajectory (1.6e-10 observed at 5 steps)
+        assert rel(g.step(5), s.step(5)) < 1e-9
+        assert rel(g.get_flat(), s.get_flat()) < 1e-8
+    finally:
+        g.close()
+        s.close()
+
+
+@pytest.mark.gpu
+def test_group_eight_ranks_c5_split_factors():
+    """Eight ranks on the full C5 problem (advection 4096^2, Matern52_Cos, Q = 30) with one
+    Kronecker factor per rank half (GPK_FLAG_SPLIT_FACTORS, the 128-wide large-factor inverse):
+    loss and full gradient vs one unsharded handle."""
+    from gpk._lib import GPK_FLAG_SPLIT_FACTORS
+    from gpk.problems import make_solver
+    from tests.test_gpu_fullsize import _config_problem, _cond_bound
+    prob, params, _, cfg = _config_problem("C5")
+    s = make_solver("C5", seed=0)
+    try:
+        assert s.inverse_path() == "big_wide"
+        s.set_params(params)
+        ls, gs = s.loss_grad()
+    finally:
+        s.close()
+    g = _group(prob, 30, cfg["freq_scale"], 8, flags=GPK_FLAG_SPLIT_FACTORS)
+    try:
+        g.set_params(params)
+        lg, gg = g.loss_grad()
+    finally:
+        g.close()
+    # row-sliced products (other tile variants, other summation order) against one handle,
+    # both without refinement: the cond(K) budget of the full-size oracle test applies
+    tol = max(1e-10, 50 * _cond_bound(prob, params) * np.finfo(float).eps)
+    assert abs(lg - ls) / abs(ls) < tol, (lg, ls)
+    assert rel(gg, gs) < tol, (rel(gg, gs), tol)
+
+
+@pytest.mark.gpu
 def test_rccl_single_rank_sharded_handle():
     """gpk_create_sharded with a one-rank RCCL communicator: the captured step with RCCL
     all-gathers / all-reduces in its graph equals the unsharded step."""

@@ -1,9 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -k "big_spd or c2_size" -x -q --timeout 120 --timeout-method thread > gpurun_out/q1_pytest.log 2>&1; rc=$?
-tail -3 gpurun_out/q1_pytest.log
-if [ $rc -ne 0 ]; then grep -E "^E |FAILED|Error" gpurun_out/q1_pytest.log | head -30; exit 1; fi
-for g in 0 255 383; do timeout -k 10 300 python tools/spd_pieces.py 2048 narrow $g > gpurun_out/q2_pieces_$g.txt 2>&1 || { cat gpurun_out/q2_pieces_$g.txt; exit 1; }; echo "G=$g"; cat gpurun_out/q2_pieces_$g.txt; done
-timeout -k 10 200 python tools/run_steps.py --config C5 --steps 10 > gpurun_out/q1_c5.txt 2>&1 || { cat gpurun_out/q1_c5.txt; exit 1; }
-head -1 gpurun_out/q1_c5.txt
+timeout -k 10 600 python -u -m pytest tests/test_shard.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/q3_pytest.log 2>&1; rc=$?
+tail -3 gpurun_out/q3_pytest.log
+if [ $rc -ne 0 ]; then grep -E "^E |FAILED|Error" gpurun_out/q3_pytest.log | head -30; exit 1; fi
