@@ -2172,3 +2172,9 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
 }
 
 }  // extern "C"
+
+// error / device helpers for the other C-ABI translation units (gpk_kron3.cpp)
+namespace gpk {
+int api_fail(int code, const std::string& msg) { return fail(code, msg); }
+int api_check_device(int dev) { return check_device(dev); }
+}  // namespace gpk

@@ -58,6 +58,18 @@ class gpk_problem(ctypes.Structure):
     ]
 
 
+class gpk_problem3(ctypes.Structure):
+    _fields_ = [
+        ("eq", ctypes.c_int32), ("kind", ctypes.c_int32),
+        ("n1", ctypes.c_int32), ("n2", ctypes.c_int32), ("n3", ctypes.c_int32), ("q", ctypes.c_int32),
+        ("x1", _dp), ("x2", _dp), ("x3", _dp), ("src", _dp), ("bvals", _dp),
+        ("jitter", ctypes.c_double), ("llk_weight", ctypes.c_double), ("logdet", ctypes.c_double),
+        ("lr", ctypes.c_double), ("b1", ctypes.c_double), ("b2", ctypes.c_double),
+        ("eps", ctypes.c_double),
+        ("device", ctypes.c_int32), ("flags", ctypes.c_int32),
+    ]
+
+
 EXPORTS = {
     "gpk_abi_version": ([], ctypes.c_int),
     "gpk_last_error": ([], ctypes.c_char_p),
@@ -100,6 +112,14 @@ EXPORTS = {
     "gpk_graph_mode": ([ctypes.c_void_p, _ip, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
     "gpk_distance_classes": ([_dp, ctypes.c_int32, _ip, _ip], ctypes.c_int),
     "gpk_class_count": ([ctypes.c_void_p, ctypes.c_int32, _ip], ctypes.c_int),
+    "gpk_create3": ([ctypes.POINTER(gpk_problem3), ctypes.c_double,
+                     ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "gpk_destroy3": ([ctypes.c_void_p], ctypes.c_int),
+    "gpk_num_params3": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
+    "gpk_set_params3": ([ctypes.c_void_p, _dp, ctypes.c_int64], ctypes.c_int),
+    "gpk_get_params3": ([ctypes.c_void_p, _dp, ctypes.c_int64], ctypes.c_int),
+    "gpk_loss_grad3": ([ctypes.c_void_p, _dp, _dp], ctypes.c_int),
+    "gpk_step3": ([ctypes.c_void_p, ctypes.c_int32, _dp], ctypes.c_int),
     "gpk_trace_reset": ([], ctypes.c_int),
     "gpk_trace_read": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                         ctypes.c_int32], ctypes.c_int),

@@ -255,6 +255,40 @@ int gpk_group_loss_grad(gpk_handle** hs, int32_t nranks, double* loss, double* g
 /* this handle's rank, group size and rows [row0, row0 + rows) of U it owns */
 int gpk_shard_info(const gpk_handle* h, int32_t* rank, int32_t* nranks, int32_t* row0, int32_t* rows);
 
+/* ---- 3-axis Kronecker solver (the d > 2 generalisation) ------------
+ * The reference's GP_solver_2d_single log joint (model_GP_solver_2d.py:87-183) with
+ * K = K1 (x) K2 (x) K3 on a tensor grid: prior -1/2 c sum_k (prod_{j!=k} N_j) logdet K_k -
+ * 1/2 <U, K^{-1} U> (the 2-axis weights :157-162), residual sum_k (D_k K_k^{-1}) x_k U - F
+ * [+ U(U^2-1)], boundary on the six faces.  Flat params (sorted-key pytree order): U
+ * [n1*n2*n3 row-major], k1.{freq, log-ls, log-w}[Q], k2..., k3..., log_tau, log_v. */
+typedef struct gpk_problem3 {
+  int32_t eq;           /* GPK_POISSON | GPK_ALLENCAHN */
+  int32_t kind;         /* GPK_SE_COS .. GPK_MATERN52 */
+  int32_t n1, n2, n3;   /* collocation points per axis */
+  int32_t q;            /* mixture components Q (1..64) */
+  const double* x1;
+  const double* x2;
+  const double* x3;
+  const double* src;    /* [n1*n2*n3] row-major */
+  const double* bvals;  /* faces U[0], U[-1], U[:,0], U[:,-1], U[:,:,0], U[:,:,-1], each row-major:
+                         * [2(n2 n3 + n1 n3 + n1 n2)] */
+  double jitter, llk_weight, logdet;
+  double lr, b1, b2, eps;
+  int32_t device;
+  int32_t flags;        /* reserved, 0 */
+} gpk_problem3;
+
+typedef struct gpk_handle3 gpk_handle3;
+int gpk_create3(const gpk_problem3* p, double freq_scale, gpk_handle3** out);
+int gpk_destroy3(gpk_handle3* h);
+int gpk_num_params3(const gpk_handle3* h, int64_t* n);
+int gpk_set_params3(gpk_handle3* h, const double* flat, int64_t n);
+int gpk_get_params3(gpk_handle3* h, double* flat, int64_t n);
+/* loss and full gradient at the current params (no update) */
+int gpk_loss_grad3(gpk_handle3* h, double* loss, double* grad_flat);
+/* n_steps of loss + gradient + Adam, device-resident; losses[n_steps] nullable */
+int gpk_step3(gpk_handle3* h, int32_t n_steps, double* losses);
+
 #ifdef __cplusplus
 }
 #endif

@@ -892,3 +892,137 @@ def train_replay_extra(prob, kind_extra, Q, freq_scale, lr, nepoch, change_point
                 break
     rec["min_err"] = min_err
     return params, pe, rec
+
+
+# ----------------------------------------------------------------------------------------
+# d = 3 Kronecker generalisation.  The reference has no 3-axis
+# solver: this restates GP_solver_2d_single's log joint (code/model_GP_solver_2d.py:87-183)
+# for K = K1 (x) K2 (x) K3 on a tensor grid U[i1, i2, i3]:
+#   prior     -1/2 c sum_k (prod_{j != k} N_j) logdet K_k  -  1/2 <U, S>,
+#             S = K1^{-1} x1 K2^{-1} x2 K3^{-1} x3 U        (the 2-axis case :157-162, :161)
+#   residual  R = sum_k (D_k K_k^{-1}) x_k U - F  [+ U(U^2 - 1)]   (U_xx, U_yy: :112, :119)
+#   boundary  the six faces U[0], U[-1], U[:,0], U[:,-1], U[:,:,0], U[:,:,-1] (the 2-axis
+#             ordering [top, bottom, left, right] of :126 extended), edges counted per face.
+# Parity against the reference is unpinned (it has no d > 2 case); the restatement is pinned
+# by torch autograd of the same formula (tests/test_oracle.py) and by its 2-axis reduction.
+# ----------------------------------------------------------------------------------------
+def _unfold(T, k):
+    """Mode-k unfolding: axis k to the front, the others flattened in order."""
+    return np.moveaxis(T, k, 0).reshape(T.shape[k], -1)
+
+
+def _fold(M, k, shape):
+    rest = [shape[j] for j in range(len(shape)) if j != k]
+    return np.moveaxis(M.reshape([shape[k]] + rest), 0, k)
+
+
+def mode_product(M, T, k):
+    """M x_k T: the mode-k product (M applied along axis k)."""
+    return _fold(M @ _unfold(T, k), k, T.shape)
+
+
+def _mode_solve(f, T, k):
+    """K_k^{-1} x_k T through the LU factors of K_k."""
+    return _fold(_solve(f, _unfold(T, k)), k, T.shape)
+
+
+def boundary_3d(U):
+    return np.concatenate([U[0].ravel(), U[-1].ravel(), U[:, 0].ravel(), U[:, -1].ravel(),
+                           U[:, :, 0].ravel(), U[:, :, -1].ravel()])
+
+
+def _boundary_scatter_3d(shape, r):
+    g = np.zeros(shape)
+    o = 0
+    for sl in ((0,), (-1,), (slice(None), 0), (slice(None), -1), (slice(None), slice(None), 0),
+               (slice(None), slice(None), -1)):
+        n = g[sl].size
+        g[sl] += r[o:o + n].reshape(g[sl].shape)
+        o += n
+    return g
+
+
+def loss_grad_3d(prob, params, want_grad=True):
+    """Negative log-joint and gradient of the 3-axis Kronecker solver.
+
+    prob keys: kind, x1, x2, x3, src [N1,N2,N3], bvals [6 faces], jitter, llk_weight, logdet,
+    eq ('poisson'|'allencahn').  params: {'U': [N1,N2,N3], 'kernel_paras_1..3', 'log_tau',
+    'log_v'} (flat order = sorted keys, as the 2-axis pytree)."""
+    kind, eq = prob["kind"], prob["eq"]
+    xs = [np.asarray(prob[f"x{a}"], np.float64).reshape(-1) for a in (1, 2, 3)]
+    Ns = tuple(x.size for x in xs)
+    Nc = Ns[0] * Ns[1] * Ns[2]
+    U = np.asarray(params["U"], np.float64).reshape(Ns)
+    kps = [params[f"kernel_paras_{a}"] for a in (1, 2, 3)]
+    log_tau, log_v = float(params["log_tau"]), float(params["log_v"])
+    tau, v = math.exp(log_tau), math.exp(log_v)
+    wb, c = float(prob["llk_weight"]), float(prob["logdet"])
+    F = np.asarray(prob["src"], np.float64).reshape(Ns)
+    bv = np.asarray(prob["bvals"], np.float64).reshape(-1)
+    Nb = bv.size
+    KD = [kernel_kd(kind, xs[k], kps[k], prob["jitter"], 2) for k in range(3)]
+    lus = [_lu(K) for K, _ in KD]
+    A = [_mode_solve(lus[k], U, k) for k in range(3)]          # K_k^{-1} x_k U
+    R = sum(mode_product(KD[k][1], A[k], k) for k in range(3)) - F
+    if eq == "allencahn":
+        R = R + U * (U * U - 1.0)
+    egap = float(np.sum(R * R))
+    S = _mode_solve(lus[2], _mode_solve(lus[1], A[0], 1), 2)
+    quad = float(np.sum(U * S))
+    lds = [_slogdet_from_lu(f) for f in lus]
+    bres = boundary_3d(U) - bv
+    bgap = float(bres @ bres)
+    log_prior = -0.5 * c * sum(Nc // Ns[k] * lds[k] for k in range(3)) - 0.5 * quad
+    log_b = 0.5 * Nb * log_tau - 0.5 * tau * bgap
+    eq_ll = 0.5 * Nc * log_v - 0.5 * v * egap
+    loss = -(log_prior + log_b * wb + eq_ll)
+    if not want_grad:
+        return loss, None
+    X = [_mode_solve(lus[k], mode_product(KD[k][1].T, R, k), k) for k in range(3)]
+    gU = S + v * (X[0] + X[1] + X[2])
+    if eq == "allencahn":
+        gU = gU + v * (3.0 * U * U - 1.0) * R
+    gU = gU + wb * tau * _boundary_scatter_3d(Ns, bres)
+    grad = {"U": gU, "log_tau": wb * (-0.5 * Nb + 0.5 * tau * bgap), "log_v": -0.5 * Nc + 0.5 * v * egap}
+    for k in range(3):
+        Kinv = _solve(lus[k], np.eye(Ns[k]))
+        Ak = _unfold(A[k], k)
+        GK = 0.5 * c * (Nc // Ns[k]) * Kinv - _unfold(0.5 * S + v * X[k], k) @ Ak.T
+        GD = v * (_unfold(R, k) @ Ak.T)
+        grad[f"kernel_paras_{k + 1}"] = param_grad_contract(kind, xs[k], kps[k], GK, GD, 2)
+    return loss, grad
+
+
+def _u3d(name):
+    s = np.sin
+    table = {
+        # a smooth mode plus a 10x finer one, per axis (a multi-scale 3-axis Poisson case)
+        "poisson_3d-mix_sin": (
+            lambda x, y, z: s(x) * s(y) * s(z) + 0.05 * s(10 * x) * s(10 * y) * s(10 * z),
+            lambda x, y, z: -3.0 * s(x) * s(y) * s(z) - 15.0 * s(10 * x) * s(10 * y) * s(10 * z)),
+        "allencahn_3d-sin": (
+            lambda x, y, z: s(2 * x) * s(2 * y) * s(2 * z),
+            lambda x, y, z: -12.0 * s(2 * x) * s(2 * y) * s(2 * z)
+            + s(2 * x) * s(2 * y) * s(2 * z) * ((s(2 * x) * s(2 * y) * s(2 * z)) ** 2 - 1.0)),
+    }
+    return table[name]
+
+
+def setup_3d(equation, n_cols, scale, kind, jitter=1e-6, llk_weight=200.0, logdet=True):
+    """A 3-axis grid (linspace(0,1,N_k) * scale per axis, as code/model_GP_solver_2d.py:369-374)
+    with the reference's boundary / source construction extended to six faces."""
+    u, src = _u3d(equation)
+    xs = [np.linspace(0, 1, num=n) * scale for n in n_cols]
+    g = np.meshgrid(*xs, indexing="ij")
+    eq = {"poisson_3d": "poisson", "allencahn_3d": "allencahn"}[equation.split("-")[0]]
+    return dict(kind=kind, x1=xs[0], x2=xs[1], x3=xs[2], src=src(*g) * np.ones_like(g[0]),
+                bvals=boundary_3d(u(*g)), jitter=jitter, llk_weight=llk_weight,
+                logdet=float(logdet), eq=eq)
+
+
+def init_params_3d(n1, n2, n3, Q, freq_scale):
+    """The 2-axis train() init (code/model_GP_solver_2d.py:245-261) with a third factor."""
+    kp = lambda: {"log-w": np.log(1 / Q) * np.ones(Q), "log-ls": np.zeros(Q),
+                  "freq": np.linspace(0, 1, Q) * freq_scale}
+    return {"log_tau": 0.0, "log_v": 0.0, "kernel_paras_1": kp(), "kernel_paras_2": kp(),
+            "kernel_paras_3": kp(), "U": np.zeros((n1, n2, n3))}

@@ -158,3 +158,35 @@ def loss_grad_1d_extra(prob, params, params_extra, kind_extra):
     loss = -(log_prior + log_boundary_ll * prob["llk_weight"] + eq_ll)
     loss.backward()
     return float(loss), _grads(tp)
+
+
+def loss_grad_3d(prob, params):
+    """The 3-axis Kronecker log joint (oracle/gp_oracle.py loss_grad_3d) written with DENSE
+    Kronecker products -- K = K1 (x) K2 (x) K3, U_xx = (D1 (x) K2 (x) K3) K^{-1} vec U, the
+    log-det of K itself -- so the oracle's mode products, unfoldings and log-det weights are
+    checked against an independent formulation (small grids only)."""
+    tp = _tp(params)
+    kind, eq = prob["kind"], prob["eq"]
+    xs = [torch.tensor(prob[f"x{a}"]) for a in (1, 2, 3)]
+    KD = [mats(kind, xs[k], tp[f"kernel_paras_{k + 1}"], prob["jitter"], 2) for k in range(3)]
+    (K1, D1), (K2, D2), (K3, D3) = KD
+    U = tp["U"]
+    u = U.reshape(-1)
+    K = torch.kron(K1, torch.kron(K2, K3))
+    Kinv_u = torch.linalg.solve(K, u)
+    lap = (torch.kron(D1, torch.kron(K2, K3)) + torch.kron(K1, torch.kron(D2, K3))
+           + torch.kron(K1, torch.kron(K2, D3))) @ Kinv_u
+    F = torch.tensor(prob["src"]).reshape(-1)
+    R = lap - F
+    if eq == "allencahn":
+        R = R + u * (u ** 2 - 1)
+    egap = (R ** 2).sum()
+    ub = torch.cat((U[0].reshape(-1), U[-1].reshape(-1), U[:, 0].reshape(-1), U[:, -1].reshape(-1),
+                    U[:, :, 0].reshape(-1), U[:, :, -1].reshape(-1)))
+    bgap = ((ub - torch.tensor(prob["bvals"])) ** 2).sum()
+    log_prior = -0.5 * torch.linalg.slogdet(K)[1] * prob["logdet"] - 0.5 * (u * Kinv_u).sum()
+    log_b = 0.5 * ub.numel() * tp["log_tau"] - 0.5 * torch.exp(tp["log_tau"]) * bgap
+    eq_ll = 0.5 * u.numel() * tp["log_v"] - 0.5 * torch.exp(tp["log_v"]) * egap
+    loss = -(log_prior + log_b * prob["llk_weight"] + eq_ll)
+    loss.backward()
+    return float(loss), _grads(tp)

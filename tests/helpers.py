@@ -35,6 +35,17 @@ def problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=24, n2=20, Q=5, seed=0, 
     return prob, params, (Xte, ute), fs
 
 
+def problem_3d(eq="poisson", kind="Matern52_Cos_1d", ns=(10, 8, 6), Q=4, seed=0, fs=5.0):
+    """A 3-axis Kronecker problem (oracle setup_3d) with seeded random params."""
+    name = {"poisson": "poisson_3d-mix_sin", "allencahn": "allencahn_3d-sin"}[eq]
+    prob = O.setup_3d(name, ns, 2 * np.pi if eq == "poisson" else 1.0, kind)
+    rng = np.random.default_rng(seed)
+    params = {"U": 0.1 * rng.normal(size=ns), "kernel_paras_1": rand_kp(rng, Q, fs),
+              "kernel_paras_2": rand_kp(rng, Q, fs), "kernel_paras_3": rand_kp(rng, Q, fs),
+              "log_tau": 0.2, "log_v": -0.1}
+    return prob, params, fs
+
+
 def device_solver(prob, Q, fs=20.0, lr=0.01, flags=0):
     from gpk.core import DeviceSolver
     if "x" in prob:

@@ -119,6 +119,61 @@ def test_loss_grad_2d_vs_autograd(kind, eq):
         assert rel(O.flatten_params(go[key]), O.flatten_params(ga[key])) < tol, key
 
 
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("eq", ["poisson", "allencahn"])
+def test_loss_grad_3d_vs_dense_kronecker_autograd(kind, eq):
+    """The 3-axis oracle (mode products, unfoldings, log-det weights, six boundary faces) vs
+    torch autograd of the same log joint written with dense Kronecker matrices."""
+    from tests.helpers import problem_3d
+    prob, params, _ = problem_3d(eq=eq, kind=kind, ns=(6, 5, 4), Q=3, seed=11)
+    lo, go = O.loss_grad_3d(prob, params)
+    la, ga = AR.loss_grad_3d(prob, params)
+    conds = [np.linalg.cond(O.kernel_matrix(kind, prob[f"x{a}"], params[f"kernel_paras_{a}"], prob["jitter"]))
+             for a in (1, 2, 3)]
+    tol = max(1e-11, 100 * float(np.prod(conds)) * np.finfo(float).eps)
+    assert abs(lo - la) / abs(la) < tol, (lo, la)
+    for key in go:
+        assert rel(O.flatten_params(go[key]), O.flatten_params(ga[key])) < tol, key
+
+
+def test_loss_grad_3d_two_axis_reduction():
+    """With a single point on axis 3 the 3-axis prior is the 2-axis one times the scalar factor
+    k3 = K3[0,0]: logdet(K1 (x) K2 (x) k3) = logdet(K1 (x) K2) + N1 N2 log k3 and
+    <U, S> = <U, S_2d> / k3 -- so the 3-axis loss equals the 2-axis loss of U / sqrt(k3)-free
+    form below (the residual of a 1-point axis has D3 = k''(0) / k3 times U)."""
+    from tests.helpers import problem_2d
+    prob2, params2, _, _ = problem_2d(eq="poisson", kind="SE_Cos_1d", n1=9, n2=7, Q=3, seed=4)
+    x3 = np.array([0.0])
+    kp3 = {"freq": np.array([0.0, 1.0, 2.0]), "log-ls": np.zeros(3), "log-w": np.log(np.ones(3) / 3)}
+    K3, D3 = O.kernel_kd(prob2["kind"], x3, kp3, prob2["jitter"], 2)
+    k3, d3 = float(K3[0, 0]), float(D3[0, 0])
+    U = params2["U"]
+    prob3 = dict(prob2, x3=x3, src=prob2["src"][:, :, None] + d3 / k3 * U[:, :, None],
+                 bvals=O.boundary_3d(np.repeat(U[:, :, None], 1, axis=2)))
+    params3 = dict(params2, U=U[:, :, None], kernel_paras_3=kp3)
+    l3, g3 = O.loss_grad_3d(prob3, params3, want_grad=True)
+    # the 2-axis log joint with the same R (the d3/k3 U term cancels against the shifted source),
+    # prior weights N3 = 1, an extra N1 N2 log k3 / 2 and <U,S> scaled by 1/k3; boundary faces:
+    # U[0], U[-1], U[:,0], U[:,-1] as in 2D plus U[:,:,0] and U[:,:,-1] = U (zero gap here)
+    prob2b = dict(prob2, bvals=O.boundary_2d(U))
+    N1, N2 = U.shape
+    l2, _ = O.loss_grad_2d(prob2b, params2, want_grad=False)
+    lds, quad = _parts_2d(prob2b, params2)
+    c = prob2["logdet"]
+    expect = l2 + 0.5 * c * N1 * N2 * np.log(k3) + 0.5 * quad * (1.0 / k3 - 1.0)
+    # boundary: 2D counts N_b = 2N1 + 2N2 faces entries, 3D adds 2 N1 N2 (all zero gap)
+    expect -= prob2["llk_weight"] * 0.5 * (2 * N1 * N2) * params2["log_tau"]
+    assert abs(l3 - expect) / abs(expect) < 1e-10, (l3, expect)
+
+
+def _parts_2d(prob, params):
+    K1 = O.kernel_matrix(prob["kind"], prob["x1"], params["kernel_paras_1"], prob["jitter"])
+    K2 = O.kernel_matrix(prob["kind"], prob["x2"], params["kernel_paras_2"], prob["jitter"])
+    U = params["U"]
+    S = np.linalg.solve(K1, U) @ np.linalg.inv(K2)
+    return (np.linalg.slogdet(K1)[1], np.linalg.slogdet(K2)[1]), float(np.sum(U * S))
+
+
 def test_loss_grad_vs_fixture():
     z = np.load(os.path.join(GOLD, "lossgrad.npz"))
     cases = {
