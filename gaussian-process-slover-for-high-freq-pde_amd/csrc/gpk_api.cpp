@@ -149,12 +149,18 @@ struct gpk_handle {
   // STEP_GRAPH_REPS training steps back to back in one graph ([0] fast, [1] full): one host
   // launch per group of steps (a graph launch boundary costs ~5-9 us of idle GPU)
   hipGraphExec_t g_multi[2] = {nullptr, nullptr};
+  // one step(1) call as one graph ([0] fast, [1] full): batch begin (snapshot, counters), the
+  // step, and the pinned-memory report -- the reference's one-call-per-iteration loop shape
+  hipGraphExec_t g_call[2] = {nullptr, nullptr};
   bool fast_ok = false;    // the fast graph exists for this handle (not row-sharded)
   int fast_mode = 0;       // next step(s) run the fast graph (gate closed with margin last time)
   long long rollbacks = 0;
   double* snap = nullptr;  // [3 * nparams] params, m, v at the start of a fast batch
   int* snap_count = nullptr;
   unsigned int* viol = nullptr;  // the fast graph met an open refinement gate
+  double* rep_host = nullptr;    // [8 + LOSS_CAP] pinned: status, viol, gates, losses (step_report)
+  double* pend_losses = nullptr; // caller's buffer for the last batch's losses (finish_batch)
+  int pend_n = 0;
   hipEvent_t ev[kMaxStages + 1] = {};
   bool profiling = false;
   int nstage = 0;
@@ -980,6 +986,45 @@ static int capture(gpk_handle* h, int apply, bool refine = true, int reps = 1) {
   return GPK_OK;
 }
 
+static StepReport make_report(gpk_handle* h, bool fast, int nloss) {
+  StepReport r{};
+  r.status = h->status;
+  r.viol = fast ? h->viol : nullptr;
+  for (int a = 0; a < h->L.naxes; ++a) r.pst[a] = h->pst[a];
+  r.out = h->rep_host;
+  r.losses = h->losses;
+  r.nloss = nloss;
+  return r;
+}
+
+// one step(1) call: begin (snapshot when fast) + step + report, captured once per graph kind
+static int capture_call(gpk_handle* h, bool fast) {
+  hipGraphExec_t* slot = &h->g_call[fast ? 0 : 1];
+  if (*slot) return GPK_OK;
+  const size_t np = (size_t)h->L.nparams;
+  hipGraph_t g = nullptr;
+  HIPCHK(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
+  StepBegin b{};
+  if (fast) {
+    b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
+    b.snap_count = h->snap_count; b.count = h->count; b.viol = h->viol;
+  }
+  b.loss_slot = h->loss_slot;
+  int rc = check_launch(launch_step_begin(b, h->s), "step_begin");
+  if (rc == GPK_OK) rc = enqueue_step(h, 1, !fast);
+  if (rc == GPK_OK) rc = check_launch(launch_step_report(make_report(h, fast, 1), h->s), "step_report");
+  hipError_t e = hipStreamEndCapture(h->s, &g);
+  if (rc != GPK_OK) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) return fail(GPK_EHIP, std::string("capture: ") + hipGetErrorString(e));
+  e = hipGraphInstantiate(slot, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) return fail(GPK_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
+  return GPK_OK;
+}
+
 static int read_status(gpk_handle* h) {
   int st = 0;
   HIPCHK(hipMemcpyAsync(&st, h->status, sizeof(int), hipMemcpyDeviceToHost, h->s));
@@ -999,15 +1044,23 @@ static int read_status(gpk_handle* h) {
 // costs one FAST_CHUNK; leaving the fast graph at the 8x margin cost ~15% on every later step
 // of C4's training, whose bound drifts into that band and stays there).
 constexpr double FAST_GRAPH_MARGIN = 8.0;
+static int read_report(gpk_handle* h, bool fast, bool* violated);
+
 static int finish_batch(gpk_handle* h, bool fast, bool* violated) {
-  int st = 0;
-  unsigned int vi = 0;
-  double ps[2][2] = {};
-  HIPCHK(hipMemcpyAsync(&st, h->status, sizeof(int), hipMemcpyDeviceToHost, h->s));
-  if (fast) HIPCHK(hipMemcpyAsync(&vi, h->viol, sizeof(unsigned int), hipMemcpyDeviceToHost, h->s));
-  for (int a = 0; a < h->L.naxes; ++a)
-    HIPCHK(hipMemcpyAsync(ps[a], h->pst[a], 2 * sizeof(double), hipMemcpyDeviceToHost, h->s));
+  TRY(check_launch(launch_step_report(make_report(h, fast, h->pend_losses ? h->pend_n : 0), h->s),
+                   "step_report"));
   HIPCHK(hipStreamSynchronize(h->s));
+  return read_report(h, fast, violated);
+}
+
+// the report written by step_report_kernel (the stream has been synchronised)
+static int read_report(gpk_handle* h, bool fast, bool* violated) {
+  if (h->pend_losses) std::memcpy(h->pend_losses, h->rep_host + 8, h->pend_n * sizeof(double));
+  h->pend_losses = nullptr;
+  h->pend_n = 0;
+  const int st = (int)h->rep_host[0];
+  const unsigned int vi = (unsigned int)h->rep_host[1];
+  double ps[2][2] = {{h->rep_host[2], h->rep_host[3]}, {h->rep_host[4], h->rep_host[5]}};
   *violated = false;
   if (st) {
     HIPCHK(hipMemsetAsync(h->status, 0, sizeof(int), h->s));
@@ -1319,6 +1372,10 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   A_(h->snap, (size_t)3 * L.nparams);
   A_(h->snap_count, 1);
   A_(h->viol, 1);
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->rep_host), (8 + LOSS_CAP) * sizeof(double),
+                    hipHostMallocCoherent) != hipSuccess)
+    return bail(fail(GPK_ENOMEM, "hipHostMalloc (step report)"));
+  std::memset(h->rep_host, 0, (8 + LOSS_CAP) * sizeof(double));
 #undef A_
   // upload the problem
   if (hipMemcpyAsync(h->x1, p->x1, L.n1 * sizeof(double), hipMemcpyHostToDevice, h->s) != hipSuccess)
@@ -1494,9 +1551,11 @@ int gpk_destroy(gpk_handle* h) {
     if (h->g_exec[k]) (void)hipGraphExecDestroy(h->g_exec[k]);
     if (h->g_fast[k]) (void)hipGraphExecDestroy(h->g_fast[k]);
     if (h->g_multi[k]) (void)hipGraphExecDestroy(h->g_multi[k]);
+    if (h->g_call[k]) (void)hipGraphExecDestroy(h->g_call[k]);
   }
   for (int k = 0; k <= kMaxStages; ++k)
     if (h->ev[k]) (void)hipEventDestroy(h->ev[k]);
+  if (h->rep_host) (void)hipHostFree(h->rep_host);
   for (void* p : h->allocs) (void)hipFree(p);
   if (h->s) (void)hipStreamDestroy(h->s);
   delete h->comm;
@@ -1562,11 +1621,16 @@ int gpk_get_opt_state(gpk_handle* h, int64_t* count, double* mu, double* nu, int
 int gpk_loss_grad(gpk_handle* h, double* loss, double* grad_flat) {
   if (!h || !loss) return fail(GPK_EINVAL, "NULL argument");
   DevSwitch ds(h->dev);
+  h->pend_losses = nullptr;
   bool fast = h->fast_ok && h->fast_mode, viol = false;
   for (int pass = 0; pass < 2; ++pass) {
     TRY(capture(h, 0, !fast));
-    if (fast) HIPCHK(hipMemsetAsync(h->viol, 0, sizeof(unsigned int), h->s));
-    HIPCHK(hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s));
+    {
+      StepBegin b{};
+      b.viol = fast ? h->viol : nullptr;
+      b.loss_slot = h->loss_slot;
+      TRY(check_launch(launch_step_begin(b, h->s), "step_begin"));
+    }
     HIPCHK(hipGraphLaunch(fast ? h->g_fast[0] : h->g_exec[0], h->s));
     HIPCHK(hipMemcpyAsync(loss, h->diag, sizeof(double), hipMemcpyDeviceToHost, h->s));
     if (grad_flat)
@@ -1579,7 +1643,7 @@ int gpk_loss_grad(gpk_handle* h, double* loss, double* grad_flat) {
   return GPK_OK;
 }
 
-static int run_steps(gpk_handle* h, int n_steps, double* losses, bool fast) {
+static int run_steps(gpk_handle* h, int n_steps, double* losses, bool fast, bool reset_slot = true) {
   hipGraphExec_t ge = fast ? h->g_fast[1] : h->g_exec[1];
   const bool multi = !h->shard && n_steps >= STEP_GRAPH_REPS;
   if (multi) TRY(capture(h, 1, !fast, STEP_GRAPH_REPS));
@@ -1587,13 +1651,17 @@ static int run_steps(gpk_handle* h, int n_steps, double* losses, bool fast) {
   int done = 0;
   while (done < n_steps) {
     const int nb = std::min(LOSS_CAP, n_steps - done);
-    HIPCHK(hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s));
+    if (reset_slot || done > 0) HIPCHK(hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s));
     int i = 0;
     if (multi)
       for (; i + STEP_GRAPH_REPS <= nb; i += STEP_GRAPH_REPS) HIPCHK(hipGraphLaunch(gm, h->s));
     for (; i < nb; ++i) HIPCHK(hipGraphLaunch(ge, h->s));
-    if (losses)
+    if (losses && done + nb < n_steps) {
       HIPCHK(hipMemcpyAsync(losses + done, h->losses, nb * sizeof(double), hipMemcpyDeviceToHost, h->s));
+    } else if (losses) {  // the last batch's losses come back with finish_batch's report
+      h->pend_losses = losses + done;
+      h->pend_n = nb;
+    }
     done += nb;
   }
   return GPK_OK;
@@ -1608,21 +1676,46 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
   if (!h) return fail(GPK_EINVAL, "NULL handle");
   if (n_steps < 0) return fail(GPK_EINVAL, "n_steps < 0");
   DevSwitch ds(h->dev);
+  h->pend_losses = nullptr;  // (a failed earlier call may have left one)
   const size_t np = (size_t)h->L.nparams, nb = np * sizeof(double);
   int done = 0;
+  if (n_steps == 1 && !h->shard) {  // one graph launch per call (a rollback takes the path below)
+    const bool fast = h->fast_ok && h->fast_mode;
+    TRY(capture_call(h, fast));
+    HIPCHK(hipGraphLaunch(h->g_call[fast ? 0 : 1], h->s));
+    HIPCHK(hipStreamSynchronize(h->s));
+    if (losses) std::memcpy(losses, h->rep_host + 8, sizeof(double));
+    bool viol = false;
+    TRY(read_report(h, fast, &viol));
+    if (!viol) return GPK_OK;
+    ++h->rollbacks;  // restore the snapshot the call graph took and rerun with the full graph
+    HIPCHK(hipMemcpyAsync(h->params, h->snap, nb, hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemcpyAsync(h->m, h->snap + np, nb, hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemcpyAsync(h->v, h->snap + 2 * np, nb, hipMemcpyDeviceToDevice, h->s));
+    HIPCHK(hipMemcpyAsync(h->count, h->snap_count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
+    TRY(check_launch(launch_sync_u(h->params, h->L, h->Up, h->s), "sync_u"));
+    TRY(capture_call(h, false));
+    HIPCHK(hipGraphLaunch(h->g_call[1], h->s));
+    HIPCHK(hipStreamSynchronize(h->s));
+    if (losses) std::memcpy(losses, h->rep_host + 8, sizeof(double));
+    return read_report(h, false, &viol);
+  }
   while (done < n_steps) {
     const bool fast = h->fast_ok && h->fast_mode;
     const int n = fast ? std::min(FAST_CHUNK, n_steps - done) : n_steps - done;
     double* lo = losses ? losses + done : nullptr;
     TRY(capture(h, 1, !fast));
-    if (fast) {  // snapshot of everything a step carries forward (Up is rebuilt from params)
-      HIPCHK(hipMemcpyAsync(h->snap, h->params, nb, hipMemcpyDeviceToDevice, h->s));
-      HIPCHK(hipMemcpyAsync(h->snap + np, h->m, nb, hipMemcpyDeviceToDevice, h->s));
-      HIPCHK(hipMemcpyAsync(h->snap + 2 * np, h->v, nb, hipMemcpyDeviceToDevice, h->s));
-      HIPCHK(hipMemcpyAsync(h->snap_count, h->count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
-      HIPCHK(hipMemsetAsync(h->viol, 0, sizeof(unsigned int), h->s));
+    {  // the snapshot of everything a fast batch carries forward (Up is rebuilt from params),
+       // the violation flag and the loss slot: one launch
+      StepBegin b{};
+      if (fast) {
+        b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
+        b.snap_count = h->snap_count; b.count = h->count; b.viol = h->viol;
+      }
+      b.loss_slot = h->loss_slot;
+      TRY(check_launch(launch_step_begin(b, h->s), "step_begin"));
     }
-    TRY(run_steps(h, n, lo, fast));
+    TRY(run_steps(h, n, lo, fast, false));
     bool viol = false;
     TRY(finish_batch(h, fast, &viol));
     if (viol) {  // a step of the chunk needed refinement: roll back and rerun with the full graph
@@ -1649,6 +1742,7 @@ int gpk_prepare(gpk_handle* h, int32_t n_steps) {
   for (int refine = 0; refine < 2; ++refine) {
     if (!refine && !h->fast_ok) continue;
     TRY(capture(h, 1, refine != 0));
+    if (!h->shard) TRY(capture_call(h, refine == 0));
     if (!h->shard && n_steps >= STEP_GRAPH_REPS) TRY(capture(h, 1, refine != 0, STEP_GRAPH_REPS));
   }
   HIPCHK(hipStreamSynchronize(h->s));

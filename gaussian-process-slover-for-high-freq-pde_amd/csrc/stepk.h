@@ -74,6 +74,21 @@ struct TailArgs {
   int tg, ngpa;              // blocks per group, groups per axis
 };
 
+struct StepBegin {
+  double* snap; const double* params; const double* m; const double* v; size_t np;
+  int* snap_count; const int* count;
+  unsigned int* viol;   // nullable
+  int* loss_slot;
+};
+struct StepReport {
+  const int* status; const unsigned int* viol;  // viol nullable
+  const double* pst[2];                         // nullable per axis
+  const double* losses; int nloss;              // the batch's losses -> out[8 ..]
+  double* out;                                  // [8 + nloss], pinned host memory
+};
+hipError_t launch_step_begin(const StepBegin& b, hipStream_t s);
+hipError_t launch_step_report(const StepReport& r, hipStream_t s);
+
 hipError_t launch_prep2(const double* params, const Layout& L, AxisConst* kc, StepScalars* sc,
                         int* count, int apply, double b1, double b2, hipStream_t s);
 hipError_t launch_reduce_parts(const double* part, int bpa, int naxes, int q, double* out,

@@ -131,4 +131,49 @@ hipError_t launch_add_into(double* dst, const double* src, size_t n, hipStream_t
   return hipGetLastError();
 }
 
+// Start of a gpk_step batch, one launch instead of five copies / memsets: the rollback snapshot
+// of params, m, v and the Adam count (snap != nullptr), the refinement-violation flag and the
+// loss-ring slot zeroed.
+__global__ __launch_bounds__(256) void step_begin_kernel(StepBegin b) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (b.snap && i < b.np) {
+    b.snap[i] = b.params[i];
+    b.snap[b.np + i] = b.m[i];
+    b.snap[2 * b.np + i] = b.v[i];
+  }
+  if (i == 0) {
+    if (b.snap) *b.snap_count = *b.count;
+    if (b.viol) *b.viol = 0u;
+    *b.loss_slot = 0;
+  }
+}
+
+hipError_t launch_step_begin(const StepBegin& b, hipStream_t s) {
+  const size_t n = b.snap ? b.np : 1;
+  hipLaunchKernelGGL(step_begin_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b);
+  return hipGetLastError();
+}
+
+// End of a batch: the status word, the violation flag, the refinement gates of both axes and the
+// batch's losses in one record written straight into pinned host memory (no device-to-host copies)
+__global__ void step_report_kernel(StepReport r) {
+  for (int k = threadIdx.x; k < r.nloss; k += blockDim.x) r.out[8 + k] = r.losses[k];
+  if (threadIdx.x != 0) {
+    __threadfence_system();
+    return;
+  }
+  r.out[0] = (double)*r.status;
+  r.out[1] = r.viol ? (double)*r.viol : 0.0;
+  for (int a = 0; a < 2; ++a) {
+    r.out[2 + 2 * a] = r.pst[a] ? r.pst[a][0] : 0.0;
+    r.out[3 + 2 * a] = r.pst[a] ? r.pst[a][1] : 0.0;  // (bits of max diag K^{-1})
+  }
+  __threadfence_system();
+}
+
+hipError_t launch_step_report(const StepReport& r, hipStream_t s) {
+  hipLaunchKernelGGL(step_report_kernel, dim3(1), dim3(256), 0, s, r);
+  return hipGetLastError();
+}
+
 }  // namespace gpk

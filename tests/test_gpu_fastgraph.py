@@ -113,3 +113,24 @@ def test_multi_step_graph_bitwise_single(name):
         assert np.array_equal(x, y)
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("name", ["2d_open", "1d_open"])
+def test_single_step_call_graph_rollback(name):
+    """step(1) runs one captured call graph (batch begin + step + pinned-memory report); a fast
+    call that meets an open gate restores the snapshot that graph took and reruns on the full
+    graph: bitwise the full-graph trajectory, call after call."""
+    from gpk._lib import GPK_FLAG_FAST_FIRST, GPK_FLAG_NO_FAST_GRAPH
+    prob, params, Q, fs = _case(name)
+    full = device_solver(prob, Q, fs, flags=GPK_FLAG_NO_FAST_GRAPH)
+    fast = device_solver(prob, Q, fs, flags=GPK_FLAG_FAST_FIRST)
+    for s in (full, fast):
+        s.set_params(params)
+    lf = [full.step(1)[0] for _ in range(3)]
+    lq = [fast.step(1)[0] for _ in range(3)]
+    assert lf == lq
+    assert fast.graph_mode() == (False, 1)
+    for a, b in zip(_state(full), _state(fast)):
+        assert np.array_equal(a, b)
+    full.close()
+    fast.close()
