@@ -57,6 +57,7 @@ struct BigSpdBatch {
   unsigned int* flag[2];
   int p[2], n[2], T[2];  // T: 64-wide tiles per dimension
   int G;                 // tile workgroups per factor in the update launch
+  int nmat;
 };
 
 __device__ __forceinline__ int bw(int p, int I) { return min(BW, p - BW * I); }
@@ -666,9 +667,24 @@ constexpr int WT = 128;
 constexpr int WIDE_LDS = 2 * 2 * huge::KS * huge::S;  // the product loop's two staging buffers
 static_assert(WIDE_LDS >= PIVOT_LDS, "the pivot reuses the staging LDS");
 
-__global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, int skip_pivot) {
+__global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, int skip_pivot, int gx,
+                                                          int per_xcd) {
   using namespace huge;
-  const int m = blockIdx.y;
+  // 1-D grid over both factors: blocks [0, nmat) are the factors' pivot workgroups (dispatched
+  // first: the pivot is the sweep's serial part); the tile workgroups after them are dealt
+  // XCD-major -- blocks t, t+8, ... share an XCD and get consecutive tiles, i.e. runs along block
+  // rows whose Z_I / Z_J panels stay in that XCD's L2.  gx = tiles per factor slot.
+  int m, x;
+  if ((int)blockIdx.x < b.nmat) {
+    m = blockIdx.x;
+    x = 0;
+  } else {
+    const int t = blockIdx.x - b.nmat;
+    const int wi = (t & 7) * per_xcd + (t >> 3);
+    if (wi >= b.nmat * gx) return;
+    m = wi / gx;
+    x = 1 + wi % gx;
+  }
   const int p = b.p[m];
   const int T2 = (p + WT - 1) / WT;  // 128-tiles per dimension
   if (k >= T2) return;
@@ -676,7 +692,6 @@ __global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, 
   const bool LAST = !has_next;  // (per factor: the factors of a batch may differ in size)
   const int nt = T2 * (T2 + 1) / 2;
   const int Q = k + 1, qlin = Q * (Q + 1) / 2 + Q;
-  const int x = blockIdx.x;
   int ti, tj;
   const bool pivot = x == 0;
   if (pivot) {
@@ -697,14 +712,14 @@ __global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, 
   const int wK = min(WT, p - WT * k);  // sweep width (a multiple of 32)
   const bool inPi = ti == k, inPj = tj == k;
   const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
-  // the tile's current values, in flight under the product (zero base in the swept blocks;
-  // clamped addresses: rows / columns past p are never stored).  Held in registers: one wave
-  // per SIMD (measured: 4.97 ms for C5's two 4096 factors, against 5.34 ms at two waves per
-  // SIMD with the base loaded in the epilogue)
+  // the tile's current values (zero base in the swept blocks; clamped addresses: rows / columns
+  // past p are never stored), held in registers (one wave per SIMD).  Vector-memory loads
+  // complete in issue order (vmcnt), so loading them up front held the first K-step's operands
+  // back behind 128 KB of HBM reads per tile: they are issued inside the product loop instead,
+  // one 16-row block at a time, each behind that K-step's operand fetch.
   double xb[4][4][4];
   const double f = (inPi || inPj) ? 0.0 : 1.0;
-#pragma unroll
-  for (int bx = 0; bx < 4; ++bx)
+  auto load_base = [&](int bx) {
 #pragma unroll
     for (int by = 0; by < 4; ++by)
 #pragma unroll
@@ -713,13 +728,34 @@ __global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, 
         const int col = min(j0 + 64 * wc + 16 * by + (lane & 15), p - 1);
         xb[bx][by][r] = X[(size_t)row * p + col] * f;
       }
+  };
   d4 acc[4][4];
 #pragma unroll
   for (int bx = 0; bx < 4; ++bx)
 #pragma unroll
     for (int by = 0; by < 4; ++by) acc[bx][by] = d4{0.0, 0.0, 0.0, 0.0};
-  // Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j])
-  product_t<1, 0>(Z, p, Z, p, wK, p, p, i0, j0, 1.0, sm, sm + 2 * KS * S, t, wr, wc, lane, acc);
+  // Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j]) -- gemm_huge_dev.h's
+  // product loop (product_t<1, 0>) with the base loads interleaved
+  {
+    constexpr int SZ = KS * S;
+    double* sA0 = sm;
+    double* sB0 = sm + 2 * SZ;
+    const int nk = wK / KS;
+    Regs R;
+    fetch<1, 0>(R, Z, p, Z, p, p, p, i0, j0, 0, t);
+    store<1, 0>(R, sA0, sB0, 1.0, t);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) fetch<1, 0>(R, Z, p, Z, p, p, p, i0, j0, (kt + 1) * KS, t);
+#pragma unroll
+      for (int bx = 0; bx < 4; ++bx)
+        if (kt == (bx * nk) / 4) load_base(bx);
+      mma(sA0 + cur * SZ, sB0 + cur * SZ, wr, wc, lane, acc);
+      if (kt + 1 < nk) store<1, 0>(R, sA0 + (cur ^ 1) * SZ, sB0 + (cur ^ 1) * SZ, 1.0, t);
+      __syncthreads();
+    }
+  }
   double mx = 0.0;
 #pragma unroll
   for (int bx = 0; bx < 4; ++bx) {
@@ -780,6 +816,7 @@ BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   // 64-wide update: 255 tile workgroups per factor (+ its pivot workgroup; two fit per CU).
   // Measured at 2048: 1177 us per inverse vs 1243 us with 383 or 511
   b.G = g_big_wgs.load() > 0 ? g_big_wgs.load() : 255;
+  b.nmat = nmat;
   for (int m = 0; m < nmat; ++m) {
     b.X[m] = a[m].X; b.Z[m] = a[m].Y; b.Li[m] = a[m].piv;
     b.ldet[m] = a[m].ldet; b.pst[m] = a[m].pst; b.status[m] = a[m].status; b.flag[m] = a[m].flag;
@@ -807,7 +844,9 @@ void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int sta
     hipLaunchKernelGGL(big_update_kernel<1>, dim3(tiles, nmat), dim3(256), 0, s, b, stage >> 1, skip_pivot);
   } else {
     const int k = stage >> 1, nsw = (Tmax + 1) / 2;
-    hipLaunchKernelGGL(wide_update_kernel, dim3(wide_tiles(Tmax), nmat), dim3(256), 0, s, b, k, skip_pivot);
+    const int gx = wide_tiles(Tmax) - 1, per_xcd = (nmat * gx + 7) / 8;
+    hipLaunchKernelGGL(wide_update_kernel, dim3(nmat + 8 * per_xcd), dim3(256), 0, s, b, k, skip_pivot, gx,
+                       per_xcd);
     // after the last sweep of every factor (a smaller factor's last sweep came earlier; later
     // launches leave it alone)
     if (k + 1 == nsw)
