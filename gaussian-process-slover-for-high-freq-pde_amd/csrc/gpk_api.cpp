@@ -124,6 +124,7 @@ struct gpk_handle {
                                       // update -> pivot hand-off counters (large path)
   bool bigspd = false;                // large-factor SPD inverse (spdinv_big.hip)
   bool bigwide = false;               // ... with 128-wide sweeps
+  double* Zp[2] = {};                 // ... its double-buffered panel [2][128][P]
   bool chain = false;                 // small factors: persistent one-launch inverse (chain_kernel)
   bool chain_aug = false;             // ... which also solves A, Bt^T and K^{-1} D^T (2D, unsharded)
   unsigned int* cflags[2] = {};       // its hand-off flags [T*(T+taug) + 2T + 1] per factor
@@ -234,6 +235,7 @@ static void fill_spd(gpk_handle* h, SpdArgs* sa) {
     sa[a].pst = h->pst[a];
     sa[a].flag = h->aflag[a];
     sa[a].wide = h->bigwide ? 1 : 0;
+    sa[a].Z = h->Zp[a];
   }
 }
 
@@ -1305,7 +1307,8 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     A_(h->ldet[a], P / 32);
     A_(h->Kc[a], (size_t)P * P);
     A_(h->pst[a], 2);
-    A_(h->aflag[a], 1);
+    A_(h->aflag[a], 4);
+    if (h->bigspd) A_(h->Zp[a], (size_t)2 * 128 * P);
     A_(h->cflags[a], (size_t)(P / 32) * (P / 32 + (P1 + P2) / 32) + 2 * (P / 32) + 1);
     if (h->chain_aug) {
       A_(h->PD[a], (size_t)P * P);

@@ -162,8 +162,9 @@ struct SpdArgs {
   double* ldet;    // [p/NB] logdet contribution of each pivot block
   double* pst;     // refinement gate [2]: K_00, bits of max diag K^{-1} (gate_open)
   int* status;     // nonzero => not positive definite
-  unsigned int* flag;  // large path: update -> pivot hand-off counter (zero-initialised)
+  unsigned int* flag;  // large path: [3] hand-off / pivot-done / panel-row counters
   int wide;        // large path: 128-wide sweeps (else 64)
+  double* Z;       // large path: double-buffered panel [2][128][p] (nullable: Y)
 };
 // Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.
 // pivot0_done: pivot block 0 was already factored (by the assembly launch).

@@ -49,12 +49,13 @@ constexpr int SS = 65;   // 64x64 LDS tile stride (doubles)
 
 struct BigSpdBatch {
   double* X[2];      // the matrix, inverted in place
-  double* Z[2];      // [W][p] panel
+  double* Z[2];      // 2 x [W][p] panel, double-buffered by sweep parity (zbuf)
   double* Li[2];     // [W][W] L^{-1} of the current pivot block (row-major, zero upper) + scratch
   double* ldet[2];   // [p/32]
   double* pst[2];    // refinement gate [2]
   int* status[2];
-  unsigned int* flag[2];
+  unsigned int* flag[2];  // [0] hand-off count (64-wide), [1] pivot done (sweep index),
+                          // [2] panel-row tiles done (cumulative over the inverse's sweeps)
   int p[2], n[2], T[2];  // T: 64-wide tiles per dimension
   int G;                 // tile workgroups per factor in the update launch
   int nmat;
@@ -286,6 +287,32 @@ __device__ __forceinline__ void pivot128(const double* src, int ld, int w, doubl
       }
 }
 
+// the panel buffer of sweep k (the update of sweep k reads it while the panel of sweep k + 1 is
+// written into the other one, by the same launch)
+template <int R>
+__device__ __forceinline__ double* zbuf(const BigSpdBatch& b, int m, int k) {
+  return b.Z[m] + (size_t)(k & 1) * (BW * R) * b.p[m];
+}
+
+// inter-workgroup hand-off (MI355X_MICROARCH §inter-workgroup visibility, plain stores + agent
+// release / acquire): every storing wave drains, barrier, one lane's release fence + counter
+__device__ __forceinline__ void release_add(unsigned int* c, unsigned int v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    atomicAdd(c, v);
+  }
+}
+__device__ __forceinline__ void acquire_wait(const unsigned int* c, unsigned int target) {
+  if (threadIdx.x == 0) {
+    while (__hip_atomic_load(const_cast<unsigned int*>(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+      __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
 // the pivot block of sweep k: 64-pivot (R = 1) or 128-pivot (R = 2)
 template <int R>
 __device__ __forceinline__ void pivot_block(const BigSpdBatch& b, int m, int k, double* sm) {
@@ -307,16 +334,18 @@ __global__ __launch_bounds__(256) void big_pivot_init_kernel(BigSpdBatch b) {
   if (threadIdx.x == 0) {
     b.pst[m][0] = x00;   // K_00 = max diag K (stationary kernel + jitter)
     b.pst[m][1] = 0.0;   // max diag K^{-1}: atomicMax'd by the last sweep
-    *b.flag[m] = 0u;
+    b.flag[m][0] = 0u;
+    b.flag[m][1] = 0u;
+    b.flag[m][2] = 0u;
   }
 }
 
 // Row block rh (64 rows) of the panel Z[:, J-block] = L^{-1} X_{P,J} (X_{P,J} of the lower
 // storage: row block P for J < P, the transpose of column block P for J > P); Z[:, P-block] =
 // L^{-1}.  L^{-1} is lower triangular: row block rh sums the column blocks kh <= rh.
+// One 256-thread workgroup, LDS sm >= 2 x 64 x 65 doubles; into zbuf(k).
 template <int R>
-__global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
-  const int m = blockIdx.y, J = blockIdx.x / R, rh = blockIdx.x % R;
+__device__ void panel_block(const BigSpdBatch& b, int m, int k, int J, int rh, double* sm) {
   const int p = b.p[m], T = b.T[m];
   const int P0 = R * k;  // first tile of the swept block
   if (P0 >= T || J >= T) return;
@@ -325,7 +354,7 @@ __global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
   const int hr = min(BW, w - BW * rh);     // rows of this output block
   const int ldl = BW * R;
   const double* X = b.X[m];
-  double* Z = b.Z[m];
+  double* Z = zbuf<R>(b, m, k);
   const double* Li = b.Li[m];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wJ = bw(p, J);
@@ -337,7 +366,8 @@ __global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
     }
     return;
   }
-  __shared__ double sL[BW * SS], sX[BW * SS];
+  double* sL = sm;
+  double* sX = sm + BW * SS;
   const int wr = wv >> 1, wc = wv & 1;
   d4 acc[2][2];
 #pragma unroll
@@ -371,6 +401,24 @@ __global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
         const int row = 32 * wr + 16 * bi + (lane >> 4) + 4 * r, col = 32 * wc + 16 * bj + (lane & 15);
         if (row < hr && col < wJ) Z[(size_t)(BW * rh + row) * p + BW * J + col] = acc[bi][bj][r];
       }
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
+  __shared__ double sm[2 * BW * SS];
+  panel_block<R>(b, blockIdx.y, k, blockIdx.x / R, blockIdx.x % R, sm);
+}
+
+// The next sweep's panel, fused into the update launch of sweep k (its last workgroups): it
+// waits for L^{-1} of pivot k + 1 (the pivot workgroup) and for the tiles of the next panel row
+// (counted by their workgroups), then fills zbuf(k + 1).  It waits only on workgroups dispatched
+// before it, none of which waits on it: no deadlock whatever the residency.
+template <int R>
+__device__ void fused_panel(const BigSpdBatch& b, int m, int k, int pj, unsigned int row_tiles, double* sm) {
+  const unsigned int* fl = b.flag[m];
+  acquire_wait(fl + 1, (unsigned)(k + 1));
+  acquire_wait(fl + 2, (unsigned)(k + 1) * row_tiles);
+  panel_block<R>(b, m, k + 1, pj / R, pj % R, sm);
 }
 
 __device__ __forceinline__ void tile_of(int lin, int& I, int& J) {
@@ -465,6 +513,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
   const int x = blockIdx.x;
   __shared__ double sm[BIG_LDS];
+  if (x > G) {  // the next sweep's panel (fused_panel); T - 1 panel-row tiles per sweep
+    const int pj = x - G - 1;
+    if (!has_next || skip_pivot || pj >= T * R) return;
+    fused_panel<R>(b, m, k, pj, (unsigned)(T - 1), sm);
+    return;
+  }
   if (x == 1) {
     if (!has_next || skip_pivot) return;
     if (threadIdx.x == 0) {  // pivot workgroup for block k+1
@@ -476,6 +530,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     __syncthreads();
     pivot_block<R>(b, m, k + 1, sm);
+    release_add(b.flag[m] + 1, 1u);  // L^{-1} of pivot k + 1 ready (fused_panel)
     return;
   }
   const int g = x == 0 ? 0 : x - 1;
@@ -483,7 +538,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int pos0 = g * chunk, pos1 = min(tl.nt, pos0 + chunk);
   if (pos0 >= pos1) return;
   double* X = b.X[m];
-  const double* Z = b.Z[m];
+  const double* Z = zbuf<R>(b, m, k);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int li = lane & 15, lk = lane >> 4;
@@ -603,6 +658,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0) atomicAdd(b.flag[m], 1u);
+      } else if (has_next && (I == R * (k + 1) || J == R * (k + 1))) {  // (R = 1) next panel row
+        release_add(b.flag[m] + 2, 1u);
       }
       if (last && I == J) {  // refinement gate: max_i (K^{-1})_ii
 #pragma unroll
@@ -675,6 +732,17 @@ __global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, 
   // XCD-major -- blocks t, t+8, ... share an XCD and get consecutive tiles, i.e. runs along block
   // rows whose Z_I / Z_J panels stay in that XCD's L2.  gx = tiles per factor slot.
   int m, x;
+  __shared__ double sm[WIDE_LDS];
+  if ((int)blockIdx.x >= b.nmat + 8 * per_xcd) {  // the next sweep's panel (fused_panel)
+    const int tmax = max(b.T[0], b.nmat > 1 ? b.T[1] : 0);
+    const int pi = blockIdx.x - b.nmat - 8 * per_xcd;
+    m = pi / (2 * tmax);
+    const int pj = pi % (2 * tmax);
+    const int T2 = (b.p[m] + WT - 1) / WT;
+    if (m >= b.nmat || k + 1 >= T2 || skip_pivot || pj >= 2 * b.T[m]) return;
+    fused_panel<2>(b, m, k, pj, (unsigned)(T2 - 1), sm);  // T2 - 1 panel-row tiles per sweep
+    return;
+  }
   if ((int)blockIdx.x < b.nmat) {
     m = blockIdx.x;
     x = 0;
@@ -703,9 +771,8 @@ __global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, 
     if (has_next && lin >= qlin) ++lin;  // (k+1, k+1) belongs to the pivot workgroup
     tile_of(lin, ti, tj);
   }
-  __shared__ double sm[WIDE_LDS];
   double* X = b.X[m];
-  const double* Z = b.Z[m];
+  const double* Z = zbuf<2>(b, m, k);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int i0 = WT * ti, j0 = WT * tj;
@@ -780,12 +847,16 @@ __global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, 
       atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
                 (unsigned long long)__double_as_longlong(mx));
   }
-  if (!pivot) return;
+  if (!pivot) {
+    if (has_next && (ti == Q || tj == Q)) release_add(b.flag[m] + 2, 1u);  // next panel row
+    return;
+  }
   // the next pivot block, factored in place from this workgroup's own stores (one L1 per
   // workgroup: visible after the barrier)
   __syncthreads();
   const int r0 = WT * Q, w = min(WT, p - r0);
   pivot128(X + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 4 * Q, b.status[m], sm);
+  release_add(b.flag[m] + 1, 1u);  // L^{-1} of pivot k + 1 ready (fused_panel)
 }
 
 // After the last 128-wide sweep: upper 64x64 tiles outside the diagonal 128 blocks <- the
@@ -818,7 +889,7 @@ BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   b.G = g_big_wgs.load() > 0 ? g_big_wgs.load() : 255;
   b.nmat = nmat;
   for (int m = 0; m < nmat; ++m) {
-    b.X[m] = a[m].X; b.Z[m] = a[m].Y; b.Li[m] = a[m].piv;
+    b.X[m] = a[m].X; b.Z[m] = a[m].Z ? a[m].Z : a[m].Y; b.Li[m] = a[m].piv;
     b.ldet[m] = a[m].ldet; b.pst[m] = a[m].pst; b.status[m] = a[m].status; b.flag[m] = a[m].flag;
     b.p[m] = a[m].p; b.n[m] = a[m].n; b.T[m] = (a[m].p + BW - 1) / BW;
     Tmax = std::max(Tmax, b.T[m]);
@@ -840,13 +911,14 @@ void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int sta
     hipLaunchKernelGGL(big_pivot_init_kernel<R>, dim3(nmat), dim3(256), 0, s, b);
   } else if ((stage & 1) == 0) {
     hipLaunchKernelGGL(big_panel_kernel<R>, dim3(Tmax * R, nmat), dim3(256), 0, s, b, stage >> 1);
-  } else if (R == 1) {
-    hipLaunchKernelGGL(big_update_kernel<1>, dim3(tiles, nmat), dim3(256), 0, s, b, stage >> 1, skip_pivot);
+  } else if (R == 1) {  // + the next sweep's panel workgroups (Tmax per factor)
+    hipLaunchKernelGGL(big_update_kernel<1>, dim3(tiles + Tmax, nmat), dim3(256), 0, s, b, stage >> 1,
+                       skip_pivot);
   } else {
     const int k = stage >> 1, nsw = (Tmax + 1) / 2;
     const int gx = wide_tiles(Tmax) - 1, per_xcd = (nmat * gx + 7) / 8;
-    hipLaunchKernelGGL(wide_update_kernel, dim3(nmat + 8 * per_xcd), dim3(256), 0, s, b, k, skip_pivot, gx,
-                       per_xcd);
+    hipLaunchKernelGGL(wide_update_kernel, dim3(nmat + 8 * per_xcd + nmat * 2 * Tmax), dim3(256), 0, s, b, k,
+                       skip_pivot, gx, per_xcd);
     // after the last sweep of every factor (a smaller factor's last sweep came earlier; later
     // launches leave it alone)
     if (k + 1 == nsw)
@@ -860,7 +932,8 @@ int spd_big_sweeps(int p, int wide) { return (p + BW * (wide ? 2 : 1) - 1) / (BW
 
 size_t spd_big_piv_doubles(int p) { return std::max<size_t>((size_t)p * 32, 128 * 128 + 2 * 64 * 64); }
 
-// stage -1: pivot 0; stage 2k: panel k; stage 2k+1: update k (profiling / bench)
+// stage -1: pivot 0; stage 2k: panel k (standalone; the inverse launches it for k = 0 only);
+// stage 2k+1: update k + the fused panel of sweep k + 1 (profiling / bench)
 hipError_t launch_spd_big_stage(SpdArgs* a, int nmat, int stage, hipStream_t s) {
   int Tmax, tiles;
   BigSpdBatch b = make_batch(a, nmat, Tmax, tiles);
@@ -884,7 +957,9 @@ hipError_t launch_spd_inverse_big(SpdArgs* a, int nmat, double** final_out, hipS
   for (int m = 0; m < nmat; ++m) final_out[m] = a[m].X;
   const int R = batch_R(a);
   const int nsw = (Tmax + R - 1) / R;
+  // pivot 0, panel 0, then one update launch per sweep (each also forms the next sweep's panel)
   for (int st = -1; st < 2 * nsw; ++st) {
+    if (st > 0 && (st & 1) == 0) continue;
     if (R == 2) launch_stage_r<2>(b, nmat, Tmax, tiles, st, s);
     else launch_stage_r<1>(b, nmat, Tmax, tiles, st, s);
   }
