@@ -753,8 +753,28 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvDesc d) {
   const int row = blockIdx.x * 4 + wv;
   double acc = 0.0;
   if (row < d.rows) {
-    const double* a = d.A + (size_t)row * d.lda;
-    for (int c = lane; c < d.p; c += 64) acc += a[c] * d.x[c];
+    // 16-B loads (p and lda are multiples of 32), 8 per lane in flight before the FMAs, four
+    // independent partial sums (a serial chain held one load round trip per 64 columns)
+    const double2* a = reinterpret_cast<const double2*>(d.A + (size_t)row * d.lda);
+    const double2* xv = reinterpret_cast<const double2*>(d.x);
+    const int n2 = d.p >> 1;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    int c = lane;
+    for (; c + 192 < n2; c += 256) {
+      double2 av[4], bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        av[u] = a[c + 64 * u];
+        bv[u] = xv[c + 64 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] = fma(av[u].y, bv[u].y, fma(av[u].x, bv[u].x, s[u]));
+    }
+    for (; c < n2; c += 64) {
+      const double2 av = a[c], bv = xv[c];
+      s[0] = fma(av.y, bv.y, fma(av.x, bv.x, s[0]));
+    }
+    acc = (s[0] + s[1]) + (s[2] + s[3]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);

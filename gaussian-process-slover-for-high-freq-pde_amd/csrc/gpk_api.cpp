@@ -124,6 +124,7 @@ struct gpk_handle {
                                       // update -> pivot hand-off counters (large path)
   bool bigspd = false;                // large-factor SPD inverse (spdinv_big.hip)
   bool bigwide = false;               // ... with 128-wide sweeps
+  bool chain_multi = false;           // persistent inverse on macro tiles (large 1D factors)
   double* Zp[2] = {};                 // ... its double-buffered panel [2][128][P]
   bool chain = false;                 // small factors: persistent one-launch inverse (chain_kernel)
   bool chain_aug = false;             // ... which also solves A, Bt^T and K^{-1} D^T (2D, unsharded)
@@ -265,6 +266,8 @@ static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin, bool au
     }
     fin[a] = h->K[a];
   }
+  if (h->chain_multi)
+    return launch_spd_chain_multi(ca, L.naxes, h->prob.eq == GPK_ADVECTION ? 1 : 2, h->s, prep, L.q);
   return launch_spd_chain(ca, L.naxes, h->prob.eq == GPK_ADVECTION ? 1 : 2, h->s, prep, L.q);
 }
 
@@ -1269,6 +1272,22 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
                grid_blocks(false) <= cap;
     h->chain_aug = h->chain && L.dim == 2 && !shard && !(p->flags & GPK_FLAG_NO_CHAIN_AUG) &&
                    grid_blocks(true) <= cap;
+    // large 1D factors: the persistent inverse on 64-row macro tiles (chain_multi_kernel), when
+    // its grid is co-resident (else the 64/128-wide launch-per-sweep path)
+    if (L.dim == 1 && !in_group && h->split_axis < 0 &&
+        !(p->flags & (GPK_FLAG_NO_CHAIN | GPK_FLAG_FORCE_BIG_SPD | GPK_FLAG_FORCE_SMALL_SPD)) &&
+        (pmax >= SPD_BIG_MIN || (p->flags & GPK_FLAG_FORCE_CHAIN_MULTI))) {
+      int mcap = g_chain_cap.load();
+      if (mcap <= 0) {
+        DevSwitch dsw(p->device);
+        const bool gather = !(p->flags & GPK_FLAG_NO_DCLASS);
+        mcap = std::min(spd_chain_multi_capacity(deriv, gather), spd_chain_multi_capacity(deriv, false));
+      }
+      if (spd_chain_multi_blocks(pp, L.naxes) <= mcap) {
+        h->chain_multi = h->chain = true;
+        h->chain_aug = h->bigspd = h->bigwide = false;
+      }
+    }
   }
   auto bail = [&](int rc) {
     gpk_destroy(h);
@@ -1808,7 +1827,9 @@ int gpk_set_chain_capacity(int32_t workgroups) {
 
 int gpk_inverse_path(const gpk_handle* h, int32_t* path) {
   if (!h || !path) return fail(GPK_EINVAL, "NULL argument");
-  *path = h->bigspd ? (h->bigwide ? GPK_INV_BIG_WIDE : GPK_INV_BIG) : h->chain_aug ? GPK_INV_CHAIN_AUG : h->chain ? GPK_INV_CHAIN : GPK_INV_SWEEP;
+  *path = h->bigspd ? (h->bigwide ? GPK_INV_BIG_WIDE : GPK_INV_BIG)
+          : h->chain_multi ? GPK_INV_CHAIN_MULTI
+          : h->chain_aug ? GPK_INV_CHAIN_AUG : h->chain ? GPK_INV_CHAIN : GPK_INV_SWEEP;
   return GPK_OK;
 }
 

@@ -223,6 +223,13 @@ __host__ __device__ inline int chain_role(int m, int x, int T, int TC) {
     if (crit(i) <= tile) ++tile;
   return tile;
 }
+// Multi-tile form for large factors (1D, p <= 2048 on a full MI355X): 64-row macro tiles of
+// the lower triangle per workgroup + the pivot chain; no augmented columns.  Co-residency as
+// above: gpk_create compares spd_chain_multi_blocks with spd_chain_multi_capacity.
+int spd_chain_multi_blocks(const int* p, int nmat);
+int spd_chain_multi_capacity(int deriv, bool gather);
+hipError_t launch_spd_chain_multi(const ChainArgs* a, int nmat, int deriv, hipStream_t s,
+                                  const PrepArgs* prep = nullptr, int q = 0);
 // prep (nullable): the step constants are published by one extra workgroup of this launch
 hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t s,
                             const PrepArgs* prep = nullptr, int q = 0);

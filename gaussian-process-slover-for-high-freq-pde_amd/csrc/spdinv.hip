@@ -264,6 +264,110 @@ __device__ __forceinline__ void load_inputs(const ChainFactor* F, double* xpre, 
   }
 }
 
+// The pivot chain of one factor (chain_kernel, chain_multi_kernel): one workgroup factors every
+// pivot block in order.  acc: this wave's quadrant of tile (0, 0) of K.  LDS: sXJ [32][SB],
+// sP / sM [32][SP], pv [32].
+__device__ __forceinline__ void chain_master(const ChainFactor& F, int T, int TC, d4 acc, double* sXJ,
+                                             double* sP, double* sM, double* pv, bool trm) {
+  const int p = F.p;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int tx = t & 31, ty = t >> 5;
+  unsigned int* panel_rdy = F.flags;
+  unsigned int* piv_rdy = F.flags + T * TC;
+  unsigned int* diag_rdy = F.flags + T * TC + T;
+    // (issue priority over the tile workgroup that may share its CU: this one is the chain)
+  __builtin_amdgcn_s_setprio(3);
+  // The pivot chain, kept in one workgroup: after factoring pivot k it holds L_k^{-1} in LDS,
+  // so pivot k+1's Schur complement X_{k+1,k+1} - V^T V (V = L_k^{-1} X_{k,k+1}) needs no hop
+  // for L_k^{-1}; its two inputs (the panel tile (k, k+1) and the diagonal tile (k+1, k+1)
+  // after sweep k-1) are published by their owners ~2 us after pivot k-1, i.e. while this
+  // workgroup is still factoring pivot k.  Same operations as the owner's update of that tile:
+  // bitwise equal.
+  // the inputs of step k (pivot k+1) are produced while pivot k is being factored: poll for
+  // them and start their loads inside that factorisation (PivotPrefetch), so they are in
+  // registers when it ends
+  double xpre[4], dpre[4];
+  __shared__ int s_pre;  // the prefetch was issued inside the factorisation
+  struct PivotPrefetch {
+    const ChainFactor* F; unsigned int *panel_rdy, *diag_rdy;
+    double *xpre, *dpre;
+    int* s_pre;
+    int k, T, TC, p, t, tx, ty, wr, wc, lane;
+    unsigned int f1, f2;
+    __device__ void early() {  // issue the flag loads; their values are looked at 3 steps later
+      f1 = f2 = 0u;
+      if (k + 1 < T && t == 0) {
+        f1 = __hip_atomic_load(panel_rdy + k * TC + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        f2 = __hip_atomic_load(diag_rdy + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __device__ void pre() {
+      if (t == 0) *s_pre = (k + 1 < T && f1 != 0u && f2 != 0u) ? 1 : 0;
+    }
+    __device__ void post() {  // both inputs published: load them (sc1) behind the barrier
+      if (!*s_pre) return;
+      load_inputs(F, xpre, dpre, k, p, tx, ty, wr, wc, lane);
+    }
+  };
+  // L^{-1}_kp is stored right after its factorisation, but its flag is raised inside the next
+  // hop (after the first product, when the stores have drained): the chain does not stall on
+  // the write-back of every pivot (the last one is signalled at once)
+  auto factor = [&](int kp) {
+    if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP + kp - 1);  // (inputs in: the hop ends)
+    store_quad(sP, SP, wr, wc, lane, acc);
+    __syncthreads();
+    if (trm && kp > 0 && kp < 17) TR_LO(SLOT_SWEEP_PIVOT + kp - 1);
+    if (trm && kp == 0) TR_LO(SLOT_PIVOT0);
+    PivotPrefetch hook{&F, panel_rdy, diag_rdy, xpre, dpre, &s_pre, kp, T, TC, p, t, tx, ty, wr, wc,
+                       lane, 0u, 0u};
+    const double ls = pivot_chol_inv_block<4, double*, PivotPrefetch>(sP, sM, pv, t, F.status, hook);
+    for (int e = t; e < 1024; e += 256) st_sc1(F.piv + (size_t)kp * 1024 + e, sM[(e >> 5) * SP + (e & 31)]);
+    if (t == 0) F.ldet[kp] = ls;
+    if (kp + 1 == T) signal_flag(piv_rdy + kp);
+    if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP_PIVOT + kp - 1);
+    if (trm && kp == 0) TR_HI(SLOT_PIVOT0);
+  };
+  // refinement gate: K_00 = max diag K (stationary kernel + jitter), and max diag K^{-1}
+  // zeroed here -- before piv_rdy[0] is raised (the vmcnt(0) ahead of that flag drains these
+  // stores), so it precedes every diagonal tile's atomicMax, which waits on all piv_rdy[k]
+  if (t == 0) {
+    st_sc1(F.pst, acc[0]);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(F.pst + 1), 0ull, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  factor(0);  // acc = tile (0, 0) of K, gathered above
+  for (int k = 0; k + 1 < T; ++k) {
+    if (trm && !s_pre) { TR_LO(SLOT_PREFETCH_MISS); TR_HI(SLOT_PREFETCH_MISS); }
+    if (!s_pre) {  // (uniform) not yet published at the prefetch point: wait and load now
+      if (t == 0) {
+        wait_flag(panel_rdy + k * TC + k + 1);
+        wait_flag(diag_rdy + k + 1);
+      }
+      __syncthreads();
+      load_inputs(&F, xpre, dpre, k, p, tx, ty, wr, wc, lane);
+    }
+    if (trm && k < 16) TR_LO(SLOT_SWEEP + k);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // prefetched during pivot k's factorisation
+      sXJ[(ty + 8 * r) * SB + tx] = xpre[r];
+      acc[r] = dpre[r];
+    }
+    __syncthreads();
+    d4 vj = {0.0, 0.0, 0.0, 0.0};
+    vj = mma_t(sM, SP, 1, sXJ, SB, 1, wr, wc, lane, vj);  // V = L_k^{-1} X_{k,k+1}
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // L^{-1}_k's stores (long drained)
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(piv_rdy + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    store_quad(sXJ, SB, wr, wc, lane, vj);
+    __syncthreads();
+    d4 prod = {0.0, 0.0, 0.0, 0.0};
+    prod = mma_t(sXJ, 1, SB, sXJ, SB, 1, wr, wc, lane, prod);  // V^T V
+    acc = acc - prod;
+    factor(k + 1);
+  }
+}
+
 template <int DERIV, bool GATHER>
 __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   const int m = blockIdx.y;
@@ -359,96 +463,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   };
   const bool trm = t == 0 && m == 0;  // probes (gpk_trace.h): factor 0's pivot owners
   if (master) {
-    // (issue priority over the tile workgroup that may share its CU: this one is the chain)
-    __builtin_amdgcn_s_setprio(3);
-    // The pivot chain, kept in one workgroup: after factoring pivot k it holds L_k^{-1} in LDS,
-    // so pivot k+1's Schur complement X_{k+1,k+1} - V^T V (V = L_k^{-1} X_{k,k+1}) needs no hop
-    // for L_k^{-1}; its two inputs (the panel tile (k, k+1) and the diagonal tile (k+1, k+1)
-    // after sweep k-1) are published by their owners ~2 us after pivot k-1, i.e. while this
-    // workgroup is still factoring pivot k.  Same operations as the owner's update of that tile:
-    // bitwise equal.
-    // the inputs of step k (pivot k+1) are produced while pivot k is being factored: poll for
-    // them and start their loads inside that factorisation (PivotPrefetch), so they are in
-    // registers when it ends
-    double xpre[4], dpre[4];
-    __shared__ int s_pre;  // the prefetch was issued inside the factorisation
-    struct PivotPrefetch {
-      const ChainFactor* F; unsigned int *panel_rdy, *diag_rdy;
-      double *xpre, *dpre;
-      int* s_pre;
-      int k, T, TC, p, t, tx, ty, wr, wc, lane;
-      unsigned int f1, f2;
-      __device__ void early() {  // issue the flag loads; their values are looked at 3 steps later
-        f1 = f2 = 0u;
-        if (k + 1 < T && t == 0) {
-          f1 = __hip_atomic_load(panel_rdy + k * TC + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          f2 = __hip_atomic_load(diag_rdy + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      __device__ void pre() {
-        if (t == 0) *s_pre = (k + 1 < T && f1 != 0u && f2 != 0u) ? 1 : 0;
-      }
-      __device__ void post() {  // both inputs published: load them (sc1) behind the barrier
-        if (!*s_pre) return;
-        load_inputs(F, xpre, dpre, k, p, tx, ty, wr, wc, lane);
-      }
-    };
-    // L^{-1}_kp is stored right after its factorisation, but its flag is raised inside the next
-    // hop (after the first product, when the stores have drained): the chain does not stall on
-    // the write-back of every pivot (the last one is signalled at once)
-    auto factor = [&](int kp) {
-      if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP + kp - 1);  // (inputs in: the hop ends)
-      store_quad(sP, SP, wr, wc, lane, acc);
-      __syncthreads();
-      if (trm && kp > 0 && kp < 17) TR_LO(SLOT_SWEEP_PIVOT + kp - 1);
-      if (trm && kp == 0) TR_LO(SLOT_PIVOT0);
-      PivotPrefetch hook{&F, panel_rdy, diag_rdy, xpre, dpre, &s_pre, kp, T, TC, p, t, tx, ty, wr, wc,
-                         lane, 0u, 0u};
-      const double ls = pivot_chol_inv_block<4, double*, PivotPrefetch>(sP, sM, pv, t, F.status, hook);
-      for (int e = t; e < 1024; e += 256) st_sc1(F.piv + (size_t)kp * 1024 + e, sM[(e >> 5) * SP + (e & 31)]);
-      if (t == 0) F.ldet[kp] = ls;
-      if (kp + 1 == T) signal_flag(piv_rdy + kp);
-      if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP_PIVOT + kp - 1);
-      if (trm && kp == 0) TR_HI(SLOT_PIVOT0);
-    };
-    // refinement gate: K_00 = max diag K (stationary kernel + jitter), and max diag K^{-1}
-    // zeroed here -- before piv_rdy[0] is raised (the vmcnt(0) ahead of that flag drains these
-    // stores), so it precedes every diagonal tile's atomicMax, which waits on all piv_rdy[k]
-    if (t == 0) {
-      st_sc1(F.pst, acc[0]);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(F.pst + 1), 0ull, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    factor(0);  // acc = tile (0, 0) of K, gathered above
-    for (int k = 0; k + 1 < T; ++k) {
-      if (trm && !s_pre) { TR_LO(SLOT_PREFETCH_MISS); TR_HI(SLOT_PREFETCH_MISS); }
-      if (!s_pre) {  // (uniform) not yet published at the prefetch point: wait and load now
-        if (t == 0) {
-          wait_flag(panel_rdy + k * TC + k + 1);
-          wait_flag(diag_rdy + k + 1);
-        }
-        __syncthreads();
-        load_inputs(&F, xpre, dpre, k, p, tx, ty, wr, wc, lane);
-      }
-      if (trm && k < 16) TR_LO(SLOT_SWEEP + k);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {  // prefetched during pivot k's factorisation
-        sXJ[(ty + 8 * r) * SB + tx] = xpre[r];
-        acc[r] = dpre[r];
-      }
-      __syncthreads();
-      d4 vj = {0.0, 0.0, 0.0, 0.0};
-      vj = mma_t(sM, SP, 1, sXJ, SB, 1, wr, wc, lane, vj);  // V = L_k^{-1} X_{k,k+1}
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // L^{-1}_k's stores (long drained)
-      __syncthreads();
-      if (t == 0) __hip_atomic_store(piv_rdy + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      store_quad(sXJ, SB, wr, wc, lane, vj);
-      __syncthreads();
-      d4 prod = {0.0, 0.0, 0.0, 0.0};
-      prod = mma_t(sXJ, 1, SB, sXJ, SB, 1, wr, wc, lane, prod);  // V^T V
-      acc = acc - prod;
-      factor(k + 1);
-    }
+    chain_master(F, T, TC, acc, sXJ, sP, sM, pv, trm);
   } else {
     if (trm && tile == 0) TR_LO(SLOT_GATHER);
     if (I == 0 && J != 0) publish_tile();  // row 0 is the panel of sweep 0
@@ -554,6 +569,315 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   }
 }
 
+// ---- multi-tile chain: large factors (1D, p up to 2048) -------------------------------------
+// chain_kernel owns one 32x32 tile per workgroup (T^2 workgroups: p <= ~700).  Here a workgroup
+// owns a LOWER macro tile -- rows {2R, 2R+1} x one pair of 32-column tiles {2C, 2C+1}, C < R - 1,
+// or, as the last workgroup of macro row R, the pair {2R-2, 2R-1} together with the diagonal
+// 2x2 block (its three lower tiles) -- so p = 2048 needs 1 + 32*31/2 = 497 workgroups + the
+// pivot chain (two per CU).  The pivot chain is chain_kernel's (chain_master); per sweep k a
+// tile workgroup:
+//   * waits for the panel tiles of its row / column pairs and L_k^{-1}, loads them (sc1);
+//   * forms V = L_k^{-1} X_{k,.} for its (up to) four tile rows / columns (MFMA, LDS);
+//   * updates its (up to) seven tiles with chain_kernel's operations -- first the tiles that
+//     feed the next sweep's panel or the pivot chain, published together (one drain + barrier),
+//     then the rest.
+// Storage is the lower triangle: panel slot (k, J) of PB holds X_{k,J} after sweep k-1; for J > k
+// it is the transpose of lower tile (J, k), published transposed by its owner.  The same
+// operation sequence per tile as chain_kernel (bitwise equal results); K^{-1} is written to both
+// triangles at the end.  V tiles are XOR-swizzled in LDS (element (k, j) at 32k + (j ^ 16(k&1)):
+// conflict-free fragment reads without padding), so the workgroup needs 42 KB.
+__device__ __forceinline__ int vsw(int k, int j) { return 32 * k + (j ^ ((k & 1) << 4)); }
+
+// acc += A B over one 32-deep product, this wave's quadrant; fa(i, k), fb(k, j) give the operands
+template <class FA, class FB>
+__device__ __forceinline__ d4 mma_f(FA fa, FB fb, int wr, int wc, int lane, d4 acc) {
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const int k = 4 * kk + lk;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa(16 * wr + li, k), fb(k, 16 * wc + li), acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// slot s of a macro-tile workgroup: s < 4 the column pair c0 (rows 2R + (s >> 1), column
+// 2 c0 + (s & 1)), s = 4..6 the diagonal block (2R,2R), (2R+1,2R), (2R+1,2R+1)
+__device__ __forceinline__ void multi_slot(int s, int R, int c0, int& I, int& J) {
+  if (s < 4) {
+    I = 2 * R + (s >> 1);
+    J = 2 * c0 + (s & 1);
+  } else {
+    I = 2 * R + (s == 4 ? 0 : 1);
+    J = 2 * R + (s == 6 ? 1 : 0);
+  }
+}
+
+// macro-tile workgroup g (0-based) -> macro row R, its column pair c0 (plain part; -1: none) and
+// whether it holds the diagonal block.  Row 0: the diagonal block only; row R >= 1: R - 1 plain
+// workgroups (c0 = 0 .. R-2), then the merged one (c0 = R-1 + diagonal).
+__host__ __device__ inline void multi_role(int g, int& R, int& c0, bool& diag) {
+  if (g == 0) {
+    R = 0; c0 = -1; diag = true;
+    return;
+  }
+  int r = 1, first = 1;  // first workgroup of macro row r: 1 + r(r-1)/2
+  while (first + r <= g) { first += r; ++r; }
+  R = r;
+  c0 = g - first;
+  diag = c0 == r - 1;
+}
+
+__host__ __device__ inline int multi_workgroups(int T) {  // per factor, + the pivot chain
+  const int MT = (T + 1) / 2;
+  return 1 + MT * (MT - 1) / 2 + 1;
+}
+
+template <int DERIV, bool GATHER>
+__global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
+  const int m = blockIdx.y;
+  if (m == b.nmat) {
+    if (blockIdx.x == 0) publish_prep(b.prep, b.q);
+    return;
+  }
+  const ChainFactor& F = b.f[m];
+  const int T = F.T, p = F.p;
+  const int nwg = multi_workgroups(T);
+  if ((int)blockIdx.x >= nwg) return;
+  const bool master = blockIdx.x == 0;
+  int R = 0, c0 = -1;
+  bool hasdiag = false;
+  if (!master) multi_role((int)blockIdx.x - 1, R, c0, hasdiag);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int tx = t & 31, ty = t >> 5;
+  unsigned int* panel_rdy = F.flags;
+  unsigned int* piv_rdy = F.flags + T * T;
+  unsigned int* diag_rdy = F.flags + T * T + T;
+  unsigned int* done = F.flags + T * T + 2 * T;
+  // LDS: L_k^{-1} [32][SA] + four swizzled V tiles; the pivot chain's sXJ / sP / sM alias them
+  __shared__ double pool[32 * SA + 4 * 1024];
+  __shared__ double pv[32];
+  __shared__ unsigned int s_last;
+  double* sL = pool;
+  double* sV = pool + 32 * SA;
+
+  auto valid = [&](int s) {
+    if (master) return false;
+    if (s < 4 && c0 < 0) return false;
+    if (s >= 4 && !hasdiag) return false;
+    int I, J;
+    multi_slot(s, R, c0, I, J);
+    return I < T && J <= I;
+  };
+  // gathered / read K value (and Kc, D written) at (i, j)
+  auto kval_at = [&](int i, int j, bool write) -> double {
+    const size_t o = (size_t)i * p + j;
+    if (GATHER) {
+      const int u = F.cid[o];
+      double kv, dv;
+      if (u >= 0) {
+        kv = F.kval[u];
+        if (i == j) kv += F.jitter;
+        dv = F.dval[u];
+        if (DERIV == 1 && !(F.x[i] - F.x[j] >= 0.0)) dv = -dv;  // JAX abs'(0) = +1
+      } else {
+        kv = (i == j) ? 1.0 : 0.0;
+        dv = 0.0;
+      }
+      if (write) {
+        if (F.Kc) F.Kc[o] = kv;
+        if (DERIV) F.D[o] = dv;
+      }
+      return kv;
+    }
+    return F.X[o];
+  };
+  d4 acc[7];
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    acc[s] = d4{0.0, 0.0, 0.0, 0.0};
+    if (!valid(s)) continue;
+    int I, J;
+    multi_slot(s, R, c0, I, J);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = I * 32 + 16 * wr + (lane >> 4) + 4 * r, j = J * 32 + 16 * wc + (lane & 15);
+      acc[s][r] = kval_at(i, j, true);
+      if (GATHER && I != J) (void)kval_at(j, i, true);  // the mirrored Kc / D entries
+    }
+  }
+  const bool trm = t == 0 && m == 0;
+  if (master) {
+    d4 a0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      a0[r] = kval_at(16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15), false);
+    double* sXJ = pool;             // [32][SB]
+    double* sP = pool + 32 * SB;    // [32][SP]
+    double* sM = sP + 32 * SP;      // [32][SP]
+    chain_master(F, T, T, a0, sXJ, sP, sM, pv, trm);
+  }
+
+  // hand-offs after sweep kk - 1 (kk = k + 1; kk = 0: before sweep 0): panel row kk -- tile
+  // (kk, J), J < kk as is, tile (I, kk), I > kk transposed -- and the diagonal tile (kk+1, kk+1)
+  // for the pivot chain.  Stores of every publishing tile of the pass, one drain + barrier, flags.
+  auto publishes = [&](int s, int kk) {
+    int I, J;
+    multi_slot(s, R, c0, I, J);
+    return (kk < T && ((I == kk && J < kk) || (J == kk && I > kk))) || (I == J && I == kk + 1);
+  };
+  auto publish = [&](int kk, bool first_pass) {
+    bool any = false;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      if (!valid(s) || !publishes(s, kk) || !first_pass) continue;
+      int I, J;
+      multi_slot(s, R, c0, I, J);
+      any = true;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
+        if (I == J)  // the pivot chain's input: the tile's own panel slot
+          st_sc1(F.PB + (size_t)(I * 32 + row) * p + I * 32 + col, acc[s][r]);
+        else if (I == kk)
+          st_sc1(F.PB + (size_t)(kk * 32 + row) * p + J * 32 + col, acc[s][r]);
+        else  // (I, kk) -> slot (kk, I) transposed
+          st_sc1(F.PB + (size_t)(kk * 32 + col) * p + I * 32 + row, acc[s][r]);
+      }
+    }
+    if (!any) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+#pragma unroll
+      for (int s = 0; s < 7; ++s) {
+        if (!valid(s) || !publishes(s, kk)) continue;
+        int I, J;
+        multi_slot(s, R, c0, I, J);
+        unsigned int* f = I == J ? diag_rdy + I : panel_rdy + kk * T + (I == kk ? J : I);
+        __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
+  if (!master) publish(0, true);
+
+  // V slots: 0, 1 = rows 2R, 2R+1; 2, 3 = the plain column pair's columns 2c0, 2c0+1
+  auto vslot_of_col = [&](int s) { return s < 4 ? 2 + (s & 1) : (s == 6 ? 1 : 0); };
+  for (int k = 0; k < T && !master; ++k) {
+    bool need[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int idx = v < 2 ? 2 * R + v : 2 * c0 + (v - 2);
+      need[v] = (v < 2 || c0 >= 0) && idx < T && idx != k;
+    }
+    if (t == 0) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        if (need[v]) wait_flag(panel_rdy + k * T + (v < 2 ? 2 * R + v : 2 * c0 + (v - 2)));
+    }
+    __syncthreads();
+    double xv[4][4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int idx = v < 2 ? 2 * R + v : 2 * c0 + (v - 2);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        xv[v][r] = need[v] ? ld_sc1(F.PB + (size_t)(k * 32 + ty + 8 * r) * p + idx * 32 + tx) : 0.0;
+    }
+    if (t == 0) wait_flag(piv_rdy + k);
+    __syncthreads();
+    const double* Li = F.piv + (size_t)k * 1024;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = ty + 8 * r;
+      sL[row * SA + tx] = ld_sc1(Li + row * 32 + tx);
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        if (need[v]) sV[v * 1024 + vsw(row, tx)] = xv[v][r];
+    }
+    __syncthreads();
+    d4 vv[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      vv[v] = d4{0.0, 0.0, 0.0, 0.0};
+      if (!need[v]) continue;
+      const double* X = sV + v * 1024;
+      vv[v] = mma_f([&](int i, int kq) { return sL[i * SA + kq]; }, [&](int kq, int j) { return X[vsw(kq, j)]; },
+                    wr, wc, lane, vv[v]);  // V = L_k^{-1} X_{k,idx}
+    }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      if (!need[v]) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        sV[v * 1024 + vsw(16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15))] = vv[v][r];
+    }
+    __syncthreads();
+    // the tiles that publish after this sweep first, then the rest
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int s = 0; s < 7; ++s) {
+        if (!valid(s) || publishes(s, k + 1) != (pass == 0)) continue;
+        int I, J;
+        multi_slot(s, R, c0, I, J);
+        const double* VI = sV + (s < 4 ? (s >> 1) : (s == 4 ? 0 : 1)) * 1024;
+        const double* VJ = sV + vslot_of_col(s) * 1024;
+        auto lt = [&](int i, int kq) { return sL[kq * SA + i]; };  // L^T (i, k) = L (k, i)
+        auto lk = [&](int kq, int j) { return sL[kq * SA + j]; };
+        auto vit = [&](int i, int kq) { return VI[vsw(kq, i)]; };  // V_I^T
+        auto vj = [&](int kq, int j) { return VJ[vsw(kq, j)]; };
+        d4 prod = {0.0, 0.0, 0.0, 0.0};
+        if (I == k && J == k) {
+          prod = mma_f(lt, lk, wr, wc, lane, prod);  // L^{-T} L^{-1}
+          acc[s] = -prod;
+        } else if (I == k) {
+          acc[s] = mma_f(lt, vj, wr, wc, lane, prod);  // L^{-T} V_J
+        } else if (J == k) {
+          acc[s] = mma_f(vit, lk, wr, wc, lane, prod);  // V_I^T L^{-1}
+        } else {
+          prod = mma_f(vit, vj, wr, wc, lane, prod);  // V_I^T V_J
+          acc[s] = acc[s] - prod;
+        }
+      }
+      if (pass == 0 && k + 1 < T) publish(k + 1, true);
+    }
+    __syncthreads();  // LDS is refilled next sweep
+  }
+  // K^{-1} = -X, both triangles; refinement gate over the diagonal tiles
+  double mx = 0.0;
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    if (!valid(s)) continue;
+    int I, J;
+    multi_slot(s, R, c0, I, J);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
+      const double y = -acc[s][r];
+      F.X[(size_t)(I * 32 + row) * p + J * 32 + col] = y;
+      if (I != J) F.X[(size_t)(J * 32 + col) * p + I * 32 + row] = y;
+      else if (row == col && I * 32 + row < F.n) mx = fmax(mx, y);
+    }
+  }
+  if (hasdiag) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0 && mx > 0.0)
+      atomicMax(reinterpret_cast<unsigned long long*>(F.pst + 1), (unsigned long long)__double_as_longlong(mx));
+  }
+  // the last workgroup of this factor re-arms the flags for the next launch
+  __syncthreads();
+  if (t == 0) s_last = atomicAdd(done, 1u) == (unsigned)(nwg - 1);
+  __syncthreads();
+  if (s_last) {
+    for (int e = t; e < T * T + 2 * T; e += 256)
+      __hip_atomic_store(F.flags + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Workgroups of chain_kernel<DERIV, GATHER> the current device keeps resident at once:
 // occupancy per CU (its VGPR / LDS footprint) x the CUs this device (or partition) exposes.
 int spd_chain_capacity(int deriv, bool gather) {
@@ -568,6 +892,26 @@ int spd_chain_capacity(int deriv, bool gather) {
   else
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, chain_kernel<2, true>, 256, 0);
   return e == hipSuccess ? per * cus : 0;
+}
+
+int spd_chain_multi_capacity(int deriv, bool gather) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  hipError_t e;
+  if (!gather)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, chain_multi_kernel<0, false>, 256, 0);
+  else if (deriv == 1)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, chain_multi_kernel<1, true>, 256, 0);
+  else
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, chain_multi_kernel<2, true>, 256, 0);
+  return e == hipSuccess ? per * cus : 0;
+}
+
+int spd_chain_multi_blocks(const int* p, int nmat) {
+  int w = 0;
+  for (int m = 0; m < nmat; ++m) w = std::max(w, multi_workgroups(p[m] / 32));
+  return w * nmat;
 }
 
 int spd_chain_blocks(const int* p, int nmat, bool aug) {
@@ -606,6 +950,35 @@ hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t
     hipLaunchKernelGGL((chain_kernel<1, true>), grid, dim3(256), 0, s, b);
   else
     hipLaunchKernelGGL((chain_kernel<2, true>), grid, dim3(256), 0, s, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_spd_chain_multi(const ChainArgs* a, int nmat, int deriv, hipStream_t s,
+                                  const PrepArgs* prep, int q) {
+  ChainBatch b{};
+  b.nmat = nmat;
+  if (prep) {
+    b.prep = *prep;
+    b.q = q;
+  }
+  int wmax = 0;
+  const bool gather = a[0].cid != nullptr;
+  for (int m = 0; m < nmat; ++m) {
+    ChainFactor& f = b.f[m];
+    f.X = a[m].X; f.PB = a[m].PB; f.piv = a[m].piv; f.ldet = a[m].ldet; f.pst = a[m].pst;
+    f.status = a[m].status; f.flags = a[m].flags; f.p = a[m].p; f.n = a[m].n; f.T = a[m].p / 32;
+    f.cid = a[m].cid; f.kval = a[m].kval; f.dval = a[m].dval; f.x = a[m].x; f.jitter = a[m].jitter;
+    f.Kc = a[m].Kc; f.D = a[m].D;
+    if ((a[m].cid != nullptr) != gather || a[m].tu || a[m].td) return hipErrorInvalidValue;
+    wmax = std::max(wmax, multi_workgroups(f.T));
+  }
+  dim3 grid(wmax, nmat + (prep ? 1 : 0));
+  if (!gather)
+    hipLaunchKernelGGL((chain_multi_kernel<0, false>), grid, dim3(256), 0, s, b);
+  else if (deriv == 1)
+    hipLaunchKernelGGL((chain_multi_kernel<1, true>), grid, dim3(256), 0, s, b);
+  else
+    hipLaunchKernelGGL((chain_multi_kernel<2, true>), grid, dim3(256), 0, s, b);
   return hipGetLastError();
 }
 

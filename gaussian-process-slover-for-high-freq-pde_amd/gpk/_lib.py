@@ -24,8 +24,9 @@ GPK_FLAG_NO_CHAIN_AUG = 256
 GPK_FLAG_FORCE_WIDE_SPD = 512
 GPK_FLAG_FORCE_NARROW_SPD = 1024
 GPK_FLAG_SPLIT_FACTORS = 2048
-GPK_INV_SWEEP, GPK_INV_CHAIN, GPK_INV_CHAIN_AUG, GPK_INV_BIG, GPK_INV_BIG_WIDE = range(5)
-INV_PATH_NAMES = {0: "sweep", 1: "chain", 2: "chain_aug", 3: "big", 4: "big_wide"}
+GPK_FLAG_FORCE_CHAIN_MULTI = 4096
+GPK_INV_SWEEP, GPK_INV_CHAIN, GPK_INV_CHAIN_AUG, GPK_INV_BIG, GPK_INV_BIG_WIDE, GPK_INV_CHAIN_MULTI = range(6)
+INV_PATH_NAMES = {0: "sweep", 1: "chain", 2: "chain_aug", 3: "big", 4: "big_wide", 5: "chain_multi"}
 KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}
 EQ_IDS = {"poisson": 0, "allencahn": 1, "advection": 2}
 

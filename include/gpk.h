@@ -111,6 +111,10 @@ typedef struct gpk_problem {
  * K2 only, and the inverses (+ their log-det blocks and refinement gates) are broadcast from
  * ranks 0 and nranks/2 -- one Kronecker factor per rank group instead of both on every rank. */
 #define GPK_FLAG_SPLIT_FACTORS 2048
+/* 1D factors of padded size >= 1600 (the large-factor range): the persistent chain inverse on
+ * 64-row macro tiles of the lower triangle, when its grid is co-resident (p <= 2048 on a full
+ * MI355X); GPK_FLAG_NO_CHAIN or GPK_FLAG_FORCE_BIG_SPD select the launch-per-sweep path. */
+#define GPK_FLAG_FORCE_CHAIN_MULTI 4096 /* the macro-tile chain at every 1D size (tests) */
 
 typedef struct gpk_handle gpk_handle;
 
@@ -145,7 +149,8 @@ int gpk_destroy(gpk_handle* h);
 /* SPD inverse path a handle's step uses (chosen at gpk_create from the factor sizes, the flags
  * and the device): 32-wide per-sweep launches, the persistent chain (K^{-1} only / augmented
  * with the first solves), or the large-factor path. */
-enum { GPK_INV_SWEEP = 0, GPK_INV_CHAIN = 1, GPK_INV_CHAIN_AUG = 2, GPK_INV_BIG = 3, GPK_INV_BIG_WIDE = 4 };
+enum { GPK_INV_SWEEP = 0, GPK_INV_CHAIN = 1, GPK_INV_CHAIN_AUG = 2, GPK_INV_BIG = 3, GPK_INV_BIG_WIDE = 4,
+       GPK_INV_CHAIN_MULTI = 5 };
 int gpk_inverse_path(const gpk_handle* h, int32_t* path);
 /* The chain's workgroups wait on one another, so gpk_create uses it only when its grid fits the
  * device's co-resident capacity (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs).  This
