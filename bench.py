@@ -62,7 +62,7 @@ def pmc_traffic(kernel):
 # ------------------------------------------------------------------------------------------
 # CPU baseline (test infrastructure: the oracle, never the product)
 # ------------------------------------------------------------------------------------------
-def cpu_baseline(config, seconds, threads, max_steps=400):
+def cpu_baseline(config, seconds, threads, max_steps=400, min_steps=1, warmup=True, blas_threads=1):
     """The CPU oracle (oracle/gp_oracle.py: NumPy/SciPy LU + OpenMP C fields) on the same
     workload, a bounded sample of `seconds` of work.  Runs in a child process of rank 0
     (`--cpu-baseline-only`): OMP / BLAS thread counts are fixed before NumPy loads."""
@@ -71,37 +71,50 @@ def cpu_baseline(config, seconds, threads, max_steps=400):
         # OpenMP (C fields) gets the cores; BLAS runs single-threaded: a multithreaded
         # OpenBLAS contending with the OpenMP pool made a 256^2 step 6x slower (measured)
         from threadpoolctl import threadpool_limits
-        threadpool_limits(limits=1, user_api="blas")
+        threadpool_limits(limits=blas_threads, user_api="blas")
     except Exception:  # pragma: no cover
         pass
     from oracle import gp_oracle as O
     from gpk.problems import CONFIGS
     cfg = CONFIGS[config]
-    prob, _, _ = O.setup_2d(cfg["equation"], cfg["n"], cfg["scale"], cfg["kernel"],
-                            llk_weight=cfg["llk_weight"], beta=cfg.get("beta"), m_test=8)
-    params = O.init_params_2d(cfg["n"], cfg["n"], 30, cfg["freq_scale"])
-    params["U"] = 0.1 * np.random.default_rng(0).normal(size=(cfg["n"], cfg["n"]))
+    n = cfg["n"]
+    if cfg["dim"] == 1:
+        prob, _, _ = O.setup_1d(cfg["equation"], n, cfg["scale"], cfg["kernel"],
+                                llk_weight=cfg["llk_weight"], m_test=8)
+        params = O.init_params_1d(n, 30, cfg["freq_scale"])
+        params["u"] = 0.1 * np.random.default_rng(0).normal(size=(n, 1))
+        loss_grad = O.loss_grad_1d
+    else:
+        prob, _, _ = O.setup_2d(cfg["equation"], n, cfg["scale"], cfg["kernel"],
+                                llk_weight=cfg["llk_weight"], beta=cfg.get("beta"), m_test=8)
+        params = O.init_params_2d(n, n, 30, cfg["freq_scale"])
+        params["U"] = 0.1 * np.random.default_rng(0).normal(size=(n, n))
+        loss_grad = O.loss_grad_2d
     opt = O.Adam(0.01)
     st = opt.init(params)
-    lo, g = O.loss_grad_2d(prob, params)          # warm-up (thread pools, page-in)
+    if warmup:
+        lo, g = loss_grad(prob, params)           # warm-up (thread pools, page-in)
     t0 = time.perf_counter()
     steps = 0
-    while steps < max_steps and (time.perf_counter() - t0) < seconds:
-        lo, g = O.loss_grad_2d(prob, params)
+    while steps < max(1, min_steps) or (steps < max_steps and (time.perf_counter() - t0) < seconds):
+        lo, g = loss_grad(prob, params)
         params, st = opt.update(g, st, params)
         steps += 1
     dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "iters/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} full steps (loss+grad+Adam) of {config} {cfg['n']}x{cfg['n']}, "
-                      f"{dt:.1f} s, oracle/gp_oracle.py (SciPy LU, 1 BLAS thread + OpenMP/libmvec "
+    return {"value": steps / dt, "unit": "iters/s", "cores": max(threads, blas_threads), "kind": "port",
+            "sample": f"{steps} full steps (loss+grad+Adam) of {config} {'x'.join([str(n)] * cfg['dim'])}, "
+                      f"{dt:.1f} s, oracle/gp_oracle.py (SciPy LU, {blas_threads} BLAS thread(s) + OpenMP/libmvec "
                       f"C fields on {threads} thread(s))"}
 
 
-def cpu_baseline_child(config, seconds, threads):
+def cpu_baseline_child(config, seconds, threads, blas_threads=1, warmup=True):
+    """blas_threads > 1: BLAS gets the cores instead of the OpenMP fields (the large configs,
+    whose step is dominated by the dense LU solves and products)."""
     env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_WAIT_POLICY="PASSIVE",
-               OPENBLAS_NUM_THREADS="1", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+               OPENBLAS_NUM_THREADS=str(blas_threads), HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--config", config,
-           "--cpu-seconds", str(seconds), "--cpu-threads", str(threads)]
+           "--cpu-seconds", str(seconds), "--cpu-threads", str(threads),
+           "--cpu-blas-threads", str(blas_threads)] + ([] if warmup else ["--cpu-no-warmup"])
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=10 * seconds + 300)
     if r.returncode != 0:
         return {"value": None, "error": r.stderr.strip().splitlines()[-1:]}
@@ -249,6 +262,8 @@ def main():
     ap.add_argument("--config", default="C4")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-blas-threads", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-no-warmup", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=50)
@@ -261,7 +276,8 @@ def main():
                     help="launcher/rank plumbing only: gloo, stand-in solver, no GPU (tests)")
     a = ap.parse_args()
     if a.cpu_baseline_only:
-        print(json.dumps(cpu_baseline(a.config, a.cpu_seconds, a.cpu_threads)), flush=True)
+        print(json.dumps(cpu_baseline(a.config, a.cpu_seconds, a.cpu_threads, warmup=not a.cpu_no_warmup,
+                                      blas_threads=a.cpu_blas_threads)), flush=True)
         return
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and a.gpus > 1:

@@ -129,6 +129,7 @@ struct gpk_handle {
   bool chain = false;                 // small factors: persistent one-launch inverse (chain_kernel)
   bool chain_aug = false;             // ... which also solves A, Bt^T and K^{-1} D^T (2D, unsharded)
   unsigned int* cflags[2] = {};       // its hand-off flags [T*(T+taug) + 2T + 1] per factor
+  double* cgran[2] = {};              // its pivot-chain input slots [T][2][1024] per factor
   double *PD[2] = {}, *PBa[2] = {};   // K_a^{-1} D_a^T; augmented panel buffers
   ClassArgs cls[2] = {};              // distance classes per axis (ncls = 0: per-pair path)
   double* rvec = nullptr;            // 1D refinement residual
@@ -248,7 +249,7 @@ static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin, bool au
   for (int a = 0; a < L.naxes; ++a) {
     ChainArgs& c = ca[a];
     c.X = h->K[a]; c.PB = h->Kb[a]; c.piv = h->piv[a]; c.ldet = h->ldet[a]; c.pst = h->pst[a];
-    c.status = h->status; c.flags = h->cflags[a];
+    c.status = h->status; c.flags = h->cflags[a]; c.gran = h->cgran[a];
     c.p = a == 0 ? L.p1 : L.p2;
     c.n = a == 0 ? L.n1 : L.n2;
     if (gather) {
@@ -1036,7 +1037,8 @@ static int read_status(gpk_handle* h) {
   HIPCHK(hipStreamSynchronize(h->s));
   if (st) {
     HIPCHK(hipMemsetAsync(h->status, 0, sizeof(int), h->s));
-    return fail(GPK_ENOTPD, "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
+    return fail(GPK_ENOTPD, (st & 2) ? "SPD inverse: a pivot-chain hand-off timed out (device status 2)"
+                                      : "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
   }
   return GPK_OK;
 }
@@ -1069,7 +1071,8 @@ static int read_report(gpk_handle* h, bool fast, bool* violated) {
   *violated = false;
   if (st) {
     HIPCHK(hipMemsetAsync(h->status, 0, sizeof(int), h->s));
-    return fail(GPK_ENOTPD, "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
+    return fail(GPK_ENOTPD, (st & 2) ? "SPD inverse: a pivot-chain hand-off timed out (device status 2)"
+                                      : "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
   }
   *violated = fast && vi;
   if (h->fast_ok) {
@@ -1329,6 +1332,13 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     A_(h->aflag[a], 4);
     if (h->bigspd) A_(h->Zp[a], (size_t)2 * 128 * P);
     A_(h->cflags[a], (size_t)(P / 32) * (P / 32 + (P1 + P2) / 32) + 2 * (P / 32) + 1);
+    A_(h->cgran[a], (size_t)(P / 32) * 2048);
+    {  // every slot starts unwritten (spdinv.hip chain_master)
+      std::vector<unsigned long long> sent((size_t)(P / 32) * 2048, CHAIN_SENTINEL);
+      if (hipMemcpyAsync(h->cgran[a], sent.data(), sent.size() * 8, hipMemcpyHostToDevice, h->s) != hipSuccess ||
+          hipStreamSynchronize(h->s) != hipSuccess)
+        return bail(fail(GPK_EHIP, "initialise the pivot-chain input slots"));
+    }
     if (h->chain_aug) {
       A_(h->PD[a], (size_t)P * P);
       A_(h->PBa[a], (size_t)P * (P1 + P2));
@@ -1780,7 +1790,7 @@ int gpk_trace_reset(void) {
 }
 
 int gpk_trace_read(uint64_t* lo, uint64_t* hi, int32_t n) {
-  if (!lo || !hi || n < TRACE_SLOTS) return fail(GPK_EINVAL, "need 128 slots");
+  if (!lo || !hi || n < TRACE_SLOTS) return fail(GPK_EINVAL, "need TRACE_SLOTS (256) slots");
   uint64_t l[4][TRACE_SLOTS], h[4][TRACE_SLOTS];
   trace_fetch_assemble(l[0], h[0]);
   trace_fetch_spdinv(l[1], h[1]);

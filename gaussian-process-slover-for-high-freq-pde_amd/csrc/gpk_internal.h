@@ -194,7 +194,11 @@ struct ChainArgs {
   double* Ou; int ldou, ou_t;              // K^{-1} B_u (stored transposed when ou_t)
   double* Od; int ldod;                    // K^{-1} D^T
   double* PBa; int ldpba;                  // augmented panel buffer [p][32*(tu+td)]
+  double* gran;                            // pivot-chain input slots [T][2][1024], CHAIN_SENTINEL
 };
+// bit pattern of an unwritten pivot-chain input word: a signalling NaN (quiet bit clear), which
+// no floating-point operation returns
+constexpr unsigned long long CHAIN_SENTINEL = 0x7ff0dead0000beefull;
 int spd_chain_blocks(const int* p, int nmat, bool aug);
 // co-resident workgroups of the chain kernel variant on the current device (0 if unknown)
 int spd_chain_capacity(int deriv, bool gather);

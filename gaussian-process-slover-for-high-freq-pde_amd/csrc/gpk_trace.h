@@ -11,7 +11,7 @@
 
 namespace gpk {
 
-constexpr int TRACE_SLOTS = 128;
+constexpr int TRACE_SLOTS = 256;
 enum TraceSlot {
   SLOT_CLASS_EVAL = 0, SLOT_GATHER = 1, SLOT_PIVOT0_WAIT = 2, SLOT_PIVOT0 = 3,
   SLOT_SWEEP = 4,         // + k (k < 16): whole sweep launch k
@@ -27,6 +27,14 @@ enum TraceSlot {
   SLOT_LAST_FLAG = 58, SLOT_LAST_LDS = 59, SLOT_LAST_MMA = 60, SLOT_LAST_OUT = 61, SLOT_LAST_AUG = 62,
   SLOT_GEMM = 64,  // + 4 * stage: first wg [start, end], + 1: first wg operands loaded,
                    // + 2: first wg MFMAs done, + 3: last wg [start, end]  (stages < 16)
+  // chain_multi_kernel, factor 0, sweep k < 16, the workgroup owning tile (k+2, k+2) (the pivot
+  // chain's next-but-one input): + k
+  SLOT_MC_PANEL = 128,  // panel tiles waited for and loads issued
+  SLOT_MC_PIV = 144,    // L_k^{-1} flag seen
+  SLOT_MC_LDS = 160,    // L_k^{-1} and panel tiles in LDS
+  SLOT_MC_V = 176,      // V products stored to LDS
+  SLOT_MC_PUB = 192,    // the pass-0 tiles published (flags raised)
+  SLOT_MC_DONE = 208,   // pass 1 done (end of the sweep)
 };
 
 #ifdef GPK_TRACE

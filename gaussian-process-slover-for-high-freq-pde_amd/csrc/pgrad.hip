@@ -151,6 +151,15 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
   const int cb = kv ? C.cbase[k] : 0;
   const int nvar = kv ? C.cbase[k + 1] - cb : 0;  // distance variants of this lane's diagonal
   const int r0 = chunk * C.rb, r1 = min(n, r0 + C.rb);
+  // variants in use by any diagonal of this wave (wave-uniform): the running sums past it are
+  // never selected, so the V-way select stops there (C2: V = 32 slots, 3-17 variants per band)
+  int nvw = V;
+  if constexpr (V > 16) {
+    nvw = nvar;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nvw = max(nvw, __shfl_xor(nvw, o, 64));
+    nvw = __builtin_amdgcn_readfirstlane(nvw);
+  }
   double ak[V], ad[V];
 #pragma unroll
   for (int x = 0; x < V; ++x) ak[x] = ad[x] = 0.0;
@@ -214,13 +223,29 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
       for (int s = 0; s < 8; ++s)
         if (!(xi[s] - xj[s] >= 0.0)) g1[s] = -g1[s];
     }
+    if constexpr (V > 16) {  // slot-major, bounded by the wave's variant count
+      int vv[8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int v = ((cv[s] - cb) & msk[s]) | ~msk[s];
+      for (int s = 0; s < 8; ++s) vv[s] = ((cv[s] - cb) & msk[s]) | ~msk[s];
 #pragma unroll
       for (int x = 0; x < V; ++x) {
-        ak[x] += (v == x) ? g0[s] : 0.0;
-        ad[x] += (v == x) ? g1[s] : 0.0;
+        if (x < nvw) {  // (uniform)
+#pragma unroll
+          for (int s = 0; s < 8; ++s) {
+            ak[x] += (vv[s] == x) ? g0[s] : 0.0;
+            ad[x] += (vv[s] == x) ? g1[s] : 0.0;
+          }
+        }
+      }
+    } else {  // (V <= 16: the unbounded pair-major form keeps C4's occupancy at 4)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int v = ((cv[s] - cb) & msk[s]) | ~msk[s];
+#pragma unroll
+        for (int x = 0; x < V; ++x) {
+          ak[x] += (v == x) ? g0[s] : 0.0;
+          ad[x] += (v == x) ? g1[s] : 0.0;
+        }
       }
     }
   }
@@ -230,8 +255,10 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
     if (w == ww) {
 #pragma unroll
       for (int x = 0; x < V; ++x) {
-        red[0][x][lane] = ww == 0 ? ak[x] : red[0][x][lane] + ak[x];
-        red[1][x][lane] = ww == 0 ? ad[x] : red[1][x][lane] + ad[x];
+        if (x < nvw) {
+          red[0][x][lane] = ww == 0 ? ak[x] : red[0][x][lane] + ak[x];
+          red[1][x][lane] = ww == 0 ? ad[x] : red[1][x][lane] + ad[x];
+        }
       }
     }
     __syncthreads();

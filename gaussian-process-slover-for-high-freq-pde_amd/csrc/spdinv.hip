@@ -215,7 +215,10 @@ struct ChainFactor {
   double* ldet;         // [T]
   double* pst;          // refinement gate [2]
   int* status;
-  unsigned int* flags;  // [T*T] panel ready, [T] pivot ready, [1] done counter (zero; re-armed)
+  unsigned int* flags;  // [T*TC] panel ready, [T] pivot ready, [T] (unused), [1] done counter
+                        // (zero; re-armed by the last workgroup)
+  double* gran;              // the pivot chain's input slots [T][2][1024] (chain_master)
+  int piv_off;               // offset of the pivot-ready flags (T * TC)
   int p, n, T;
   // gather mode: K from the distance classes (+ jitter), kept copy Kc and D written on the way
   const int* cid; const double* kval; const double* dval; const double* x; double jitter;
@@ -233,6 +236,7 @@ struct ChainBatch {
   int nmat;
   PrepArgs prep;  // published by workgroup (0, nmat) when the grid has that extra row
   int q;
+  int mpos;       // chain_multi_kernel: linear index of the pivot chain's workgroup
 };
 
 __device__ __forceinline__ void st_sc1(double* p, double v) {
@@ -252,62 +256,61 @@ __device__ __forceinline__ void signal_flag(unsigned int* f) {
   if (threadIdx.x == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// the pivot chain's inputs for pivot k+1: panel tile (k, k+1) (LDS-staging layout) and the
-// diagonal tile (k+1, k+1) (MFMA quadrant layout), both after sweep k-1, sc1 loads
-__device__ __forceinline__ void load_inputs(const ChainFactor* F, double* xpre, double* dpre, int k,
-                                            int p, int tx, int ty, int wr, int wc, int lane) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    xpre[r] = ld_sc1(F->PB + (size_t)(k * 32 + ty + 8 * r) * p + (k + 1) * 32 + tx);
-    dpre[r] = ld_sc1(F->PB + (size_t)((k + 1) * 32 + 16 * wr + (lane >> 4) + 4 * r) * p + (k + 1) * 32 +
-                     16 * wc + (lane & 15));  // the diagonal tile's slot
-  }
+// The pivot chain's inputs travel as self-validating words (MI355X_MICROARCH.md hand-off row
+// handoff-1to1; cdna_hip_programming.md Guideline 16 R2 with the data as its own flag): every
+// fp64 element is ONE 8-byte sc1 store into a slot that holds a sentinel (a signalling-NaN bit
+// pattern, which no floating-point operation produces: results are quieted) until it is
+// written.  The producer neither drains its stores nor raises a flag; the pivot chain, the
+// slot's only reader, loads the words, re-loads any that still hold the sentinel, and after
+// consuming a slot writes the sentinel back (ready for the next launch; the buffer is
+// initialised to the sentinel at create, gpk_api.cpp).  Slot k (hop k, the inputs of pivot
+// k+1): [0] panel tile (k, k+1), [1] diagonal tile (k+1, k+1), both after sweep k-1; element
+// e = 32 row + col of the tile.
+__device__ __forceinline__ double* gran_at(const ChainFactor& F, int slot, int which, int e) {
+  return F.gran + (size_t)(2 * slot + which) * 1024 + e;
+}
+__device__ __forceinline__ bool gran_ok(double v) {
+  return __double_as_longlong(v) != (long long)CHAIN_SENTINEL;
 }
 
 // The pivot chain of one factor (chain_kernel, chain_multi_kernel): one workgroup factors every
 // pivot block in order.  acc: this wave's quadrant of tile (0, 0) of K.  LDS: sXJ [32][SB],
 // sP / sM [32][SP], pv [32].
-__device__ __forceinline__ void chain_master(const ChainFactor& F, int T, int TC, d4 acc, double* sXJ,
-                                             double* sP, double* sM, double* pv, bool trm) {
-  const int p = F.p;
+__device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc, double* sXJ,
+                                             double* sP, double* sM, double* pv, bool trm,
+                                             bool early_flag) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int tx = t & 31, ty = t >> 5;
-  unsigned int* panel_rdy = F.flags;
-  unsigned int* piv_rdy = F.flags + T * TC;
-  unsigned int* diag_rdy = F.flags + T * TC + T;
+  unsigned int* piv_rdy = F.flags + F.piv_off;
     // (issue priority over the tile workgroup that may share its CU: this one is the chain)
   __builtin_amdgcn_s_setprio(3);
   // The pivot chain, kept in one workgroup: after factoring pivot k it holds L_k^{-1} in LDS,
   // so pivot k+1's Schur complement X_{k+1,k+1} - V^T V (V = L_k^{-1} X_{k,k+1}) needs no hop
   // for L_k^{-1}; its two inputs (the panel tile (k, k+1) and the diagonal tile (k+1, k+1)
-  // after sweep k-1) are published by their owners ~2 us after pivot k-1, i.e. while this
+  // after sweep k-1) are handed over (self-validating words, above) by their owners while this
   // workgroup is still factoring pivot k.  Same operations as the owner's update of that tile:
-  // bitwise equal.
-  // the inputs of step k (pivot k+1) are produced while pivot k is being factored: poll for
-  // them and start their loads inside that factorisation (PivotPrefetch), so they are in
-  // registers when it ends
-  double xpre[4], dpre[4];
-  __shared__ int s_pre;  // the prefetch was issued inside the factorisation
+  // bitwise equal.  Their loads are issued inside that factorisation (PivotPrefetch, after block
+  // step 5) and checked after it; words that were not yet written are re-loaded.
+  // element of this thread: panel tile (LDS-staging layout: row ty + 8r, column tx) and the
+  // diagonal tile (MFMA quadrant layout)
+  auto ex = [&](int r) { return (ty + 8 * r) * 32 + tx; };
+  auto ed = [&](int r) { return (16 * wr + (lane >> 4) + 4 * r) * 32 + 16 * wc + (lane & 15); };
+  double gx[4], gd[4];
+  auto issue = [&](int k) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      gx[r] = ld_sc1(gran_at(F, k, 0, ex(r)));
+      gd[r] = ld_sc1(gran_at(F, k, 1, ed(r)));
+    }
+  };
   struct PivotPrefetch {
-    const ChainFactor* F; unsigned int *panel_rdy, *diag_rdy;
-    double *xpre, *dpre;
-    int* s_pre;
-    int k, T, TC, p, t, tx, ty, wr, wc, lane;
-    unsigned int f1, f2;
-    __device__ void early() {  // issue the flag loads; their values are looked at 3 steps later
-      f1 = f2 = 0u;
-      if (k + 1 < T && t == 0) {
-        f1 = __hip_atomic_load(panel_rdy + k * TC + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        f2 = __hip_atomic_load(diag_rdy + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __device__ void pre() {
-      if (t == 0) *s_pre = (k + 1 < T && f1 != 0u && f2 != 0u) ? 1 : 0;
-    }
-    __device__ void post() {  // both inputs published: load them (sc1) behind the barrier
-      if (!*s_pre) return;
-      load_inputs(F, xpre, dpre, k, p, tx, ty, wr, wc, lane);
+    decltype(issue)* f;
+    int k, T;
+    __device__ void early() {}
+    __device__ void pre() {}
+    __device__ void post() {
+      if (k + 1 < T) (*f)(k);
     }
   };
   // L^{-1}_kp is stored right after its factorisation, but its flag is raised inside the next
@@ -319,8 +322,7 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, int TC
     __syncthreads();
     if (trm && kp > 0 && kp < 17) TR_LO(SLOT_SWEEP_PIVOT + kp - 1);
     if (trm && kp == 0) TR_LO(SLOT_PIVOT0);
-    PivotPrefetch hook{&F, panel_rdy, diag_rdy, xpre, dpre, &s_pre, kp, T, TC, p, t, tx, ty, wr, wc,
-                       lane, 0u, 0u};
+    PivotPrefetch hook{&issue, kp, T};
     const double ls = pivot_chol_inv_block<4, double*, PivotPrefetch>(sP, sM, pv, t, F.status, hook);
     for (int e = t; e < 1024; e += 256) st_sc1(F.piv + (size_t)kp * 1024 + e, sM[(e >> 5) * SP + (e & 31)]);
     if (t == 0) F.ldet[kp] = ls;
@@ -338,27 +340,43 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, int TC
   }
   factor(0);  // acc = tile (0, 0) of K, gathered above
   for (int k = 0; k + 1 < T; ++k) {
-    if (trm && !s_pre) { TR_LO(SLOT_PREFETCH_MISS); TR_HI(SLOT_PREFETCH_MISS); }
-    if (!s_pre) {  // (uniform) not yet published at the prefetch point: wait and load now
-      if (t == 0) {
-        wait_flag(panel_rdy + k * TC + k + 1);
-        wait_flag(diag_rdy + k + 1);
+    // L_k's flag: raised inside the hop (below); with early_flag (chain_multi, whose inputs are
+    // usually late) at once -- its stores drain while the inputs are awaited, and the tile
+    // workgroups' sweep k (which produces pivot k+2's inputs) does not wait for this hop
+    if (early_flag) signal_flag(piv_rdy + k);
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ok = ok && gran_ok(gx[r]) && gran_ok(gd[r]);
+    if (trm && !ok) { TR_LO(SLOT_PREFETCH_MISS); TR_HI(SLOT_PREFETCH_MISS); }  // (thread 0's words)
+    // (per lane) words not yet written when they were loaded: load them again.  Bounded: a
+    // hand-off that never arrives flags the status word (the step reports an error) instead of
+    // hanging the device.
+    for (unsigned spins = 0; !ok; ++spins) {
+      if (spins == (1u << 22)) {
+        atomicOr(F.status, 2);
+        break;
       }
-      __syncthreads();
-      load_inputs(&F, xpre, dpre, k, p, tx, ty, wr, wc, lane);
+      __builtin_amdgcn_s_sleep(1);
+      issue(k);
+      ok = true;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ok = ok && gran_ok(gx[r]) && gran_ok(gd[r]);
     }
     if (trm && k < 16) TR_LO(SLOT_SWEEP + k);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {  // prefetched during pivot k's factorisation
-      sXJ[(ty + 8 * r) * SB + tx] = xpre[r];
-      acc[r] = dpre[r];
+      sXJ[(ty + 8 * r) * SB + tx] = gx[r];
+      acc[r] = gd[r];
+      // consumed: the sentinel back into the slot for the next launch
+      st_sc1(gran_at(F, k, 0, ex(r)), __longlong_as_double((long long)CHAIN_SENTINEL));
+      st_sc1(gran_at(F, k, 1, ed(r)), __longlong_as_double((long long)CHAIN_SENTINEL));
     }
     __syncthreads();
     d4 vj = {0.0, 0.0, 0.0, 0.0};
     vj = mma_t(sM, SP, 1, sXJ, SB, 1, wr, wc, lane, vj);  // V = L_k^{-1} X_{k,k+1}
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // L^{-1}_k's stores (long drained)
     __syncthreads();
-    if (t == 0) __hip_atomic_store(piv_rdy + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0 && !early_flag) __hip_atomic_store(piv_rdy + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     store_quad(sXJ, SB, wr, wc, lane, vj);
     __syncthreads();
     d4 prod = {0.0, 0.0, 0.0, 0.0};
@@ -391,7 +409,6 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   const int tx = t & 31, ty = t >> 5;
   unsigned int* panel_rdy = F.flags;
   unsigned int* piv_rdy = F.flags + T * TC;
-  unsigned int* diag_rdy = F.flags + T * TC + T;
   unsigned int* done = F.flags + T * TC + 2 * T;
   // panel tile (row k) of column J: K part in PB, augmented part in PBa
   auto panel_ptr = [&](int k, int row, int col) -> double* {
@@ -453,21 +470,22 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     for (int r = 0; r < 4; ++r) st_sc1(panel_ptr(I, 16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15)), acc[r]);
     signal_flag(panel_rdy + I * TC + J);
   };
-  // diagonal tile (I, I) as it is after sweep I-2, for the pivot chain's workgroup: stored in
-  // its own panel slot (I, I) of PB, which the panel of sweep I overwrites only after the chain
-  // has consumed it (that publication needs pivot I, which needs this tile)
-  auto publish_diag = [&](void) {
+  // the pivot chain's inputs of hop kk (after sweep kk-1): panel tile (kk, kk+1) and diagonal
+  // tile (kk+1, kk+1) as granules (chain_master), before any other store of the tile
+  auto chain_inputs = [&](int kk) {
+    const int which = (I == kk && J == kk + 1) ? 0 : (I == J && I == kk + 1) ? 1 : -1;
+    if (which < 0 || kk + 1 >= T) return;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) st_sc1(panel_ptr(I, 16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15)), acc[r]);
-    signal_flag(diag_rdy + I);
+    for (int r = 0; r < 4; ++r)
+      st_sc1(gran_at(F, kk, which, (16 * wr + (lane >> 4) + 4 * r) * 32 + 16 * wc + (lane & 15)), acc[r]);
   };
   const bool trm = t == 0 && m == 0;  // probes (gpk_trace.h): factor 0's pivot owners
   if (master) {
-    chain_master(F, T, TC, acc, sXJ, sP, sM, pv, trm);
+    chain_master(F, T, acc, sXJ, sP, sM, pv, trm, false);
   } else {
     if (trm && tile == 0) TR_LO(SLOT_GATHER);
+    chain_inputs(0);                       // tiles (0, 1) and (1, 1) as they are before sweep 0
     if (I == 0 && J != 0) publish_tile();  // row 0 is the panel of sweep 0
-    if (I == 1 && J == 1 && T > 1) publish_diag();  // tile (1, 1) as it is before sweep 0
   }
 
   for (int k = 0; k < T && !master; ++k) {
@@ -522,8 +540,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     }
     // panel of sweep k + 1 (the diagonal tile's panel slot is the pivot chain's: nobody reads
     // a (k, k) panel tile)
+    chain_inputs(k + 1);  // tiles (k+1, k+2), (k+2, k+2) after sweep k: pivot k+2's inputs
     if (k + 1 < T && I == k + 1 && J != I) publish_tile();
-    if (I == J && I == k + 2) publish_diag();  // tile (k+2, k+2) after sweep k, for pivot k + 2
     if (trl) TR_HI(SLOT_LAST_MMA);
     __syncthreads();  // LDS is refilled next sweep
   }
@@ -643,16 +661,18 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
   const int T = F.T, p = F.p;
   const int nwg = multi_workgroups(T);
   if ((int)blockIdx.x >= nwg) return;
-  const bool master = blockIdx.x == 0;
+  // the pivot chain's workgroup sits at linear index mpos (host: a CU the dispatcher's second
+  // pass over the CUs does not double up), the tile workgroups around it
+  const int mpos = b.mpos < nwg ? b.mpos : 0;
+  const bool master = (int)blockIdx.x == mpos;
   int R = 0, c0 = -1;
   bool hasdiag = false;
-  if (!master) multi_role((int)blockIdx.x - 1, R, c0, hasdiag);
+  if (!master) multi_role((int)blockIdx.x - ((int)blockIdx.x > mpos ? 1 : 0), R, c0, hasdiag);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int tx = t & 31, ty = t >> 5;
   unsigned int* panel_rdy = F.flags;
   unsigned int* piv_rdy = F.flags + T * T;
-  unsigned int* diag_rdy = F.flags + T * T + T;
   unsigned int* done = F.flags + T * T + 2 * T;
   // LDS: L_k^{-1} [32][SA] + four swizzled V tiles; the pivot chain's sXJ / sP / sM alias them
   __shared__ double pool[32 * SA + 4 * 1024];
@@ -715,36 +735,60 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
     double* sXJ = pool;             // [32][SB]
     double* sP = pool + 32 * SB;    // [32][SP]
     double* sM = sP + 32 * SP;      // [32][SP]
-    chain_master(F, T, T, a0, sXJ, sP, sM, pv, trm);
+    chain_master(F, T, a0, sXJ, sP, sM, pv, trm, true);
   }
 
   // hand-offs after sweep kk - 1 (kk = k + 1; kk = 0: before sweep 0): panel row kk -- tile
-  // (kk, J), J < kk as is, tile (I, kk), I > kk transposed -- and the diagonal tile (kk+1, kk+1)
-  // for the pivot chain.  Stores of every publishing tile of the pass, one drain + barrier, flags.
+  // (kk, J), J < kk as is, tile (I, kk), I > kk transposed (stores of every publishing tile of
+  // the pass, one drain + barrier, flags) -- and, as granules first, the pivot chain's inputs of
+  // hop kk: tile (kk+1, kk) (= panel tile (kk, kk+1) transposed) and the diagonal tile
+  // (kk+1, kk+1)
   auto publishes = [&](int s, int kk) {
     int I, J;
     multi_slot(s, R, c0, I, J);
-    return (kk < T && ((I == kk && J < kk) || (J == kk && I > kk))) || (I == J && I == kk + 1);
+    return kk < T && ((I == kk && J < kk) || (J == kk && I > kk));
   };
-  auto publish = [&](int kk, bool first_pass) {
+  auto chain_in = [&](int s, int kk) {
+    int I, J;
+    multi_slot(s, R, c0, I, J);
+    return kk + 1 < T && I == kk + 1 && (J == kk || J == I);
+  };
+  // stores of every publishing tile (sc1, not waited for here)
+  auto publish_stores = [&](int kk) {
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      if (!valid(s) || !chain_in(s, kk)) continue;
+      int I, J;
+      multi_slot(s, R, c0, I, J);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
+        if (I == J)
+          st_sc1(gran_at(F, kk, 1, row * 32 + col), acc[s][r]);
+        else  // (kk+1, kk) -> element (col, row) of panel tile (kk, kk+1)
+          st_sc1(gran_at(F, kk, 0, col * 32 + row), acc[s][r]);
+      }
+    }
     bool any = false;
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
-      if (!valid(s) || !publishes(s, kk) || !first_pass) continue;
+      if (!valid(s) || !publishes(s, kk)) continue;
       int I, J;
       multi_slot(s, R, c0, I, J);
       any = true;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
-        if (I == J)  // the pivot chain's input: the tile's own panel slot
-          st_sc1(F.PB + (size_t)(I * 32 + row) * p + I * 32 + col, acc[s][r]);
-        else if (I == kk)
+        if (I == kk)
           st_sc1(F.PB + (size_t)(kk * 32 + row) * p + J * 32 + col, acc[s][r]);
         else  // (I, kk) -> slot (kk, I) transposed
           st_sc1(F.PB + (size_t)(kk * 32 + col) * p + I * 32 + row, acc[s][r]);
       }
     }
+    return any;
+  };
+  // every wave's stores drained, a barrier, then one lane raises the flags
+  auto publish_flags = [&](int kk, bool any) {
     if (!any) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -754,16 +798,18 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
         if (!valid(s) || !publishes(s, kk)) continue;
         int I, J;
         multi_slot(s, R, c0, I, J);
-        unsigned int* f = I == J ? diag_rdy + I : panel_rdy + kk * T + (I == kk ? J : I);
+        unsigned int* f = panel_rdy + kk * T + (I == kk ? J : I);
         __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   };
-  if (!master) publish(0, true);
+  if (!master) publish_flags(0, publish_stores(0));
 
   // V slots: 0, 1 = rows 2R, 2R+1; 2, 3 = the plain column pair's columns 2c0, 2c0+1
   auto vslot_of_col = [&](int s) { return s < 4 ? 2 + (s & 1) : (s == 6 ? 1 : 0); };
   for (int k = 0; k < T && !master; ++k) {
+    // probes (gpk_trace.h SLOT_MC_*): the workgroup owning tile (k+2, k+2), factor 0
+    const bool trc = t == 0 && m == 0 && hasdiag && k < 16 && (k + 2 == 2 * R || k + 2 == 2 * R + 1);
     bool need[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -784,7 +830,9 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
       for (int r = 0; r < 4; ++r)
         xv[v][r] = need[v] ? ld_sc1(F.PB + (size_t)(k * 32 + ty + 8 * r) * p + idx * 32 + tx) : 0.0;
     }
+    if (trc) TR_HI(SLOT_MC_PANEL + k);
     if (t == 0) wait_flag(piv_rdy + k);
+    if (trc) TR_HI(SLOT_MC_PIV + k);
     __syncthreads();
     const double* Li = F.piv + (size_t)k * 1024;
 #pragma unroll
@@ -796,6 +844,7 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
         if (need[v]) sV[v * 1024 + vsw(row, tx)] = xv[v][r];
     }
     __syncthreads();
+    if (trc) TR_HI(SLOT_MC_LDS + k);
     d4 vv[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -814,12 +863,15 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
         sV[v * 1024 + vsw(16 * wr + (lane >> 4) + 4 * r, 16 * wc + (lane & 15))] = vv[v][r];
     }
     __syncthreads();
-    // the tiles that publish after this sweep first, then the rest
+    if (trc) TR_HI(SLOT_MC_V + k);
+    // the tiles that publish after this sweep first (stores, drain, flags), then the rest.
+    // (Updating the rest while the stores drain, flags after it, was measured slower: the drain
+    // does not shorten behind MFMA work, so the flags came later.)
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
       for (int s = 0; s < 7; ++s) {
-        if (!valid(s) || publishes(s, k + 1) != (pass == 0)) continue;
+        if (!valid(s) || (publishes(s, k + 1) || chain_in(s, k + 1)) != (pass == 0)) continue;
         int I, J;
         multi_slot(s, R, c0, I, J);
         const double* VI = sV + (s < 4 ? (s >> 1) : (s == 4 ? 0 : 1)) * 1024;
@@ -841,9 +893,11 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
           acc[s] = acc[s] - prod;
         }
       }
-      if (pass == 0 && k + 1 < T) publish(k + 1, true);
+      if (pass == 0 && k + 1 < T) publish_flags(k + 1, publish_stores(k + 1));
+      if (pass == 0 && trc) TR_HI(SLOT_MC_PUB + k);
     }
     __syncthreads();  // LDS is refilled next sweep
+    if (trc) TR_HI(SLOT_MC_DONE + k);
   }
   // K^{-1} = -X, both triangles; refinement gate over the diagonal tiles
   double mx = 0.0;
@@ -940,7 +994,8 @@ hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t
     f.tu = a[m].tu; f.td = a[m].td; f.Bu = a[m].Bu; f.ldbu = a[m].ldbu; f.bu_t = a[m].bu_t;
     f.Ou = a[m].Ou; f.ldou = a[m].ldou; f.ou_t = a[m].ou_t; f.Od = a[m].Od; f.ldod = a[m].ldod;
     f.PBa = a[m].PBa; f.ldpba = a[m].ldpba;
-    if ((a[m].cid != nullptr) != gather) return hipErrorInvalidValue;
+    f.gran = a[m].gran; f.piv_off = f.T * (f.T + f.tu + f.td);
+    if ((a[m].cid != nullptr) != gather || !f.gran) return hipErrorInvalidValue;
     Tmax = std::max(Tmax, f.T * (f.T + f.tu + f.td) + 1);  // + the pivot chain's workgroup
   }
   dim3 grid(Tmax, nmat + (prep ? 1 : 0));
@@ -969,9 +1024,20 @@ hipError_t launch_spd_chain_multi(const ChainArgs* a, int nmat, int deriv, hipSt
     f.status = a[m].status; f.flags = a[m].flags; f.p = a[m].p; f.n = a[m].n; f.T = a[m].p / 32;
     f.cid = a[m].cid; f.kval = a[m].kval; f.dval = a[m].dval; f.x = a[m].x; f.jitter = a[m].jitter;
     f.Kc = a[m].Kc; f.D = a[m].D;
-    if ((a[m].cid != nullptr) != gather || a[m].tu || a[m].td) return hipErrorInvalidValue;
+    f.gran = a[m].gran; f.piv_off = f.T * f.T;
+    if ((a[m].cid != nullptr) != gather || a[m].tu || a[m].td || !f.gran)
+      return hipErrorInvalidValue;
     wmax = std::max(wmax, multi_workgroups(f.T));
   }
+  // one factor: the pivot chain in the middle of the CUs that hold a single workgroup (the
+  // dispatcher deals the first `cus` workgroups one per CU, the rest double up the first CUs
+  // again; placement only -- the flags order everything)
+  b.mpos = 0;
+  int dev = 0, cus = 0;
+  if (nmat == 1 && hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      wmax > cus && wmax < 2 * cus)
+    b.mpos = wmax - cus + (2 * cus - wmax) / 2;
   dim3 grid(wmax, nmat + (prep ? 1 : 0));
   if (!gather)
     hipLaunchKernelGGL((chain_multi_kernel<0, false>), grid, dim3(256), 0, s, b);

@@ -14,6 +14,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "gaussian-process-slover-for-high-freq-pde_amd")]
 import numpy as np
 
+NS = 256  # gpk_trace.h TRACE_SLOTS
+
 # single-workgroup probes (gpk_trace.h): "first" = workgroup 0, "last" = the last in the grid
 NAMES = {0: "class_eval first wg", 1: "gather pivot wg | chain wg(0,0)", 2: "pivot0 wait done", 3: "pivot0 factor",
          40: "class_sum first wg", 41: "pgrad first wg start", 42: "pg first wg contracted",
@@ -30,6 +32,13 @@ for k in range(16):
     NAMES[66 + 4 * k] = f"  gemm {k} first wg mfma done"
     NAMES[67 + 4 * k] = f"  gemm {k} last wg"
 for k in range(16):
+    NAMES[128 + k] = f"mc sweep {k}: panel loads issued"
+    NAMES[144 + k] = f"mc sweep {k}: L flag seen"
+    NAMES[160 + k] = f"mc sweep {k}: L + panel in LDS"
+    NAMES[176 + k] = f"mc sweep {k}: V in LDS"
+    NAMES[192 + k] = f"mc sweep {k}: pass-0 published"
+    NAMES[208 + k] = f"mc sweep {k}: sweep done"
+for k in range(16):
     NAMES[4 + k] = f"sweep {k} (pivot wg)"
     NAMES[20 + k] = f"  pivot in sweep {k}"
 
@@ -45,24 +54,24 @@ from gpk import _lib, problems  # noqa: E402
 lib = _lib.load()
 s = problems.make_solver(a.config, seed=0)
 s.step(20)
-U64 = ctypes.c_uint64 * 128
-acc_lo, acc_hi, cnt = np.zeros(128), np.zeros(128), np.zeros(128)
+U64 = ctypes.c_uint64 * NS
+acc_lo, acc_hi, cnt = np.zeros(NS), np.zeros(NS), np.zeros(NS)
 for _ in range(a.steps):
     _lib.check(lib.gpk_trace_reset())
     s.step(1)
     lo, hi = U64(), U64()
-    _lib.check(lib.gpk_trace_read(lo, hi, 128))
+    _lib.check(lib.gpk_trace_read(lo, hi, NS))
     lo = np.array(lo[:], dtype=np.float64)
     hi = np.array(hi[:], dtype=np.float64)
     valid_lo = lo < 2 ** 63
     t0 = lo[valid_lo].min()
-    for i in range(128):
+    for i in range(NS):
         if hi[i] > 0 or valid_lo[i]:
             acc_lo[i] += (lo[i] - t0) / 100.0 if valid_lo[i] else np.nan
             acc_hi[i] += (hi[i] - t0) / 100.0 if hi[i] > 0 else np.nan
             cnt[i] += 1
 print(f"{a.config}: one step, device timeline (us, mean of {a.steps})")
-for i in sorted(range(128), key=lambda i: (acc_lo[i] / max(cnt[i], 1)) if cnt[i] and not np.isnan(acc_lo[i]) else 1e9):
+for i in sorted(range(NS), key=lambda i: (acc_lo[i] / max(cnt[i], 1)) if cnt[i] and not np.isnan(acc_lo[i]) else 1e9):
     if cnt[i]:
         l, h = acc_lo[i] / cnt[i], acc_hi[i] / cnt[i]
         print(f"  {str(NAMES.get(i, i)):24s} {l:9.2f} .. {h:9.2f}   ({h - l:7.2f})")
