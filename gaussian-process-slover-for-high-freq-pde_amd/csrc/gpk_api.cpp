@@ -130,6 +130,8 @@ struct gpk_handle {
   bool chain_aug = false;             // ... which also solves A, Bt^T and K^{-1} D^T (2D, unsharded)
   unsigned int* cflags[2] = {};       // its hand-off flags [T*(T+taug) + 2T + 1] per factor
   double* cgran[2] = {};              // its pivot-chain input slots [T][2][1024] per factor
+  double* PB2[2] = {};                // chain_multi: panel slots [2][P*P] by launch parity
+  unsigned int* cepoch[2] = {};       // chain_multi: launch counter per factor
   double *PD[2] = {}, *PBa[2] = {};   // K_a^{-1} D_a^T; augmented panel buffers
   ClassArgs cls[2] = {};              // distance classes per axis (ncls = 0: per-pair path)
   double* rvec = nullptr;            // 1D refinement residual
@@ -250,6 +252,7 @@ static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin, bool au
     ChainArgs& c = ca[a];
     c.X = h->K[a]; c.PB = h->Kb[a]; c.piv = h->piv[a]; c.ldet = h->ldet[a]; c.pst = h->pst[a];
     c.status = h->status; c.flags = h->cflags[a]; c.gran = h->cgran[a];
+    c.PB2 = h->PB2[a]; c.epoch = h->cepoch[a];
     c.p = a == 0 ? L.p1 : L.p2;
     c.n = a == 0 ? L.n1 : L.n2;
     if (gather) {
@@ -1333,11 +1336,14 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     if (h->bigspd) A_(h->Zp[a], (size_t)2 * 128 * P);
     A_(h->cflags[a], (size_t)(P / 32) * (P / 32 + (P1 + P2) / 32) + 2 * (P / 32) + 1);
     A_(h->cgran[a], (size_t)(P / 32) * 2048);
-    {  // every slot starts unwritten (spdinv.hip chain_master)
-      std::vector<unsigned long long> sent((size_t)(P / 32) * 2048, CHAIN_SENTINEL);
-      if (hipMemcpyAsync(h->cgran[a], sent.data(), sent.size() * 8, hipMemcpyHostToDevice, h->s) != hipSuccess ||
-          hipStreamSynchronize(h->s) != hipSuccess)
-        return bail(fail(GPK_EHIP, "initialise the pivot-chain input slots"));
+    // every hand-off slot starts unwritten (spdinv.hip chain_master / chain_multi_kernel)
+    if (hipMemsetD32Async(h->cgran[a], CHAIN_SENTINEL32, (size_t)(P / 32) * 4096, h->s) != hipSuccess)
+      return bail(fail(GPK_EHIP, "initialise the pivot-chain input slots"));
+    if (h->chain_multi) {
+      A_(h->PB2[a], (size_t)2 * P * P);
+      A_(h->cepoch[a], 4);
+      if (hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, (size_t)4 * P * P, h->s) != hipSuccess)
+        return bail(fail(GPK_EHIP, "initialise the panel slots"));
     }
     if (h->chain_aug) {
       A_(h->PD[a], (size_t)P * P);

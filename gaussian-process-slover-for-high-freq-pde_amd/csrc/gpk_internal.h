@@ -195,10 +195,13 @@ struct ChainArgs {
   double* Od; int ldod;                    // K^{-1} D^T
   double* PBa; int ldpba;                  // augmented panel buffer [p][32*(tu+td)]
   double* gran;                            // pivot-chain input slots [T][2][1024], CHAIN_SENTINEL
+  double* PB2; unsigned int* epoch;        // chain_multi: panel slots [2][p*p] (CHAIN_SENTINEL),
+                                           // launch counter (zeroed)
 };
-// bit pattern of an unwritten pivot-chain input word: a signalling NaN (quiet bit clear), which
-// no floating-point operation returns
-constexpr unsigned long long CHAIN_SENTINEL = 0x7ff0dead0000beefull;
+// bit pattern of an unwritten hand-off word: a signalling NaN (quiet bit clear), which no
+// floating-point operation returns; equal 32-bit halves (hipMemsetD32 fills it)
+constexpr unsigned long long CHAIN_SENTINEL = 0x7ff4dead7ff4deadull;
+constexpr unsigned int CHAIN_SENTINEL32 = 0x7ff4deadu;
 int spd_chain_blocks(const int* p, int nmat, bool aug);
 // co-resident workgroups of the chain kernel variant on the current device (0 if unknown)
 int spd_chain_capacity(int deriv, bool gather);

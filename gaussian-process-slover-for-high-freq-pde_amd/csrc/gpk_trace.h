@@ -35,6 +35,7 @@ enum TraceSlot {
   SLOT_MC_V = 176,      // V products stored to LDS
   SLOT_MC_PUB = 192,    // the pass-0 tiles published (flags raised)
   SLOT_MC_DONE = 208,   // pass 1 done (end of the sweep)
+  SLOT_MC_PROD = 224,   // pass-0 products done (before their stores)
 };
 
 #ifdef GPK_TRACE

@@ -218,6 +218,8 @@ struct ChainFactor {
   unsigned int* flags;  // [T*TC] panel ready, [T] pivot ready, [T] (unused), [1] done counter
                         // (zero; re-armed by the last workgroup)
   double* gran;              // the pivot chain's input slots [T][2][1024] (chain_master)
+  double* PB2;               // chain_multi: panel slots [2][p*p] by launch parity (self-validating)
+  unsigned int* epoch;       // chain_multi: launch counter (its parity selects the PB2 half)
   int piv_off;               // offset of the pivot-ready flags (T * TC)
   int p, n, T;
   // gather mode: K from the distance classes (+ jitter), kept copy Kc and D written on the way
@@ -671,9 +673,14 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int tx = t & 31, ty = t >> 5;
-  unsigned int* panel_rdy = F.flags;
   unsigned int* piv_rdy = F.flags + T * T;
   unsigned int* done = F.flags + T * T + 2 * T;
+  // panel hand-off: self-validating words (chain_master's inputs, above) in the PB2 half of this
+  // launch's parity; the other half (last launch's) is reset to the sentinel meanwhile, a chunk
+  // per tile workgroup and sweep, off the critical path.  No flags, no drains.
+  const unsigned ep = __hip_atomic_load(F.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double* PBc = F.PB2 + (size_t)(ep & 1u) * p * p;
+  double* PBo = F.PB2 + (size_t)((ep & 1u) ^ 1u) * p * p;
   // LDS: L_k^{-1} [32][SA] + four swizzled V tiles; the pivot chain's sXJ / sP / sM alias them
   __shared__ double pool[32 * SA + 4 * 1024];
   __shared__ double pv[32];
@@ -769,41 +776,28 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
           st_sc1(gran_at(F, kk, 0, col * 32 + row), acc[s][r]);
       }
     }
-    bool any = false;
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
       if (!valid(s) || !publishes(s, kk)) continue;
       int I, J;
       multi_slot(s, R, c0, I, J);
-      any = true;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
         if (I == kk)
-          st_sc1(F.PB + (size_t)(kk * 32 + row) * p + J * 32 + col, acc[s][r]);
+          st_sc1(PBc + (size_t)(kk * 32 + row) * p + J * 32 + col, acc[s][r]);
         else  // (I, kk) -> slot (kk, I) transposed
-          st_sc1(F.PB + (size_t)(kk * 32 + col) * p + I * 32 + row, acc[s][r]);
-      }
-    }
-    return any;
-  };
-  // every wave's stores drained, a barrier, then one lane raises the flags
-  auto publish_flags = [&](int kk, bool any) {
-    if (!any) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-#pragma unroll
-      for (int s = 0; s < 7; ++s) {
-        if (!valid(s) || !publishes(s, kk)) continue;
-        int I, J;
-        multi_slot(s, R, c0, I, J);
-        unsigned int* f = panel_rdy + kk * T + (I == kk ? J : I);
-        __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          st_sc1(PBc + (size_t)(kk * 32 + col) * p + I * 32 + row, acc[s][r]);
       }
     }
   };
-  if (!master) publish_flags(0, publish_stores(0));
+  if (!master) publish_stores(0);
+  // this workgroup's share of the other half's reset: [rs0, rs1), a chunk per sweep
+  const size_t ntot = (size_t)p * p;
+  const int gidx = (int)blockIdx.x - ((int)blockIdx.x > mpos ? 1 : 0);
+  const size_t share = (ntot + (nwg - 2)) / (nwg - 1);
+  const size_t rs0 = std::min(ntot, (size_t)gidx * share), rs1 = std::min(ntot, rs0 + share);
+  const size_t rchunk = (share + T - 1) / T;
 
   // V slots: 0, 1 = rows 2R, 2R+1; 2, 3 = the plain column pair's columns 2c0, 2c0+1
   auto vslot_of_col = [&](int s) { return s < 4 ? 2 + (s & 1) : (s == 6 ? 1 : 0); };
@@ -816,19 +810,33 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
       const int idx = v < 2 ? 2 * R + v : 2 * c0 + (v - 2);
       need[v] = (v < 2 || c0 >= 0) && idx < T && idx != k;
     }
-    if (t == 0) {
+    // panel tiles of sweep k: load, re-load the words still holding the sentinel (bounded)
+    double xv[4][4];
+    auto load_panel = [&]() {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int idx = v < 2 ? 2 * R + v : 2 * c0 + (v - 2);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          xv[v][r] = need[v] ? ld_sc1(PBc + (size_t)(k * 32 + ty + 8 * r) * p + idx * 32 + tx) : 0.0;
+      }
+    };
+    auto panel_ok = [&]() {
+      bool ok = true;
 #pragma unroll
       for (int v = 0; v < 4; ++v)
-        if (need[v]) wait_flag(panel_rdy + k * T + (v < 2 ? 2 * R + v : 2 * c0 + (v - 2)));
-    }
-    __syncthreads();
-    double xv[4][4];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int idx = v < 2 ? 2 * R + v : 2 * c0 + (v - 2);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        xv[v][r] = need[v] ? ld_sc1(F.PB + (size_t)(k * 32 + ty + 8 * r) * p + idx * 32 + tx) : 0.0;
+        for (int r = 0; r < 4; ++r) ok = ok && gran_ok(xv[v][r]);
+      return ok;
+    };
+    load_panel();
+    for (unsigned spins = 0; !panel_ok(); ++spins) {
+      if (spins == (1u << 22)) {
+        atomicOr(F.status, 2);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      load_panel();
     }
     if (trc) TR_HI(SLOT_MC_PANEL + k);
     if (t == 0) wait_flag(piv_rdy + k);
@@ -864,9 +872,10 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
     }
     __syncthreads();
     if (trc) TR_HI(SLOT_MC_V + k);
-    // the tiles that publish after this sweep first (stores, drain, flags), then the rest.
-    // (Updating the rest while the stores drain, flags after it, was measured slower: the drain
-    // does not shorten behind MFMA work, so the flags came later.)
+    // the tiles that publish after this sweep (and the pivot chain's inputs) first, their
+    // stores, then the rest.  (Forming V_I^T V_J as P_I^T (M_k P_J), M_k = L_k^{-T} L_k^{-1},
+    // halves the V products but moved no sweep: the critical merged workgroups keep 4 products,
+    // and the 5-step C2 trajectory drifted past the oracle budget -- measured, reverted.)
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
@@ -893,8 +902,14 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
           acc[s] = acc[s] - prod;
         }
       }
-      if (pass == 0 && k + 1 < T) publish_flags(k + 1, publish_stores(k + 1));
+      if (pass == 0 && trc) TR_HI(SLOT_MC_PROD + k);
+      if (pass == 0 && k + 1 < T) publish_stores(k + 1);
       if (pass == 0 && trc) TR_HI(SLOT_MC_PUB + k);
+    }
+    {  // reset chunk k of this workgroup's share of the other half
+      const size_t b0 = rs0 + (size_t)k * rchunk, b1 = std::min(rs1, b0 + rchunk);
+      for (size_t e = b0 + t; e < b1; e += 256)
+        PBo[e] = __longlong_as_double((long long)CHAIN_SENTINEL);
     }
     __syncthreads();  // LDS is refilled next sweep
     if (trc) TR_HI(SLOT_MC_DONE + k);
@@ -929,6 +944,7 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
     for (int e = t; e < T * T + 2 * T; e += 256)
       __hip_atomic_store(F.flags + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(F.epoch, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1024,8 +1040,8 @@ hipError_t launch_spd_chain_multi(const ChainArgs* a, int nmat, int deriv, hipSt
     f.status = a[m].status; f.flags = a[m].flags; f.p = a[m].p; f.n = a[m].n; f.T = a[m].p / 32;
     f.cid = a[m].cid; f.kval = a[m].kval; f.dval = a[m].dval; f.x = a[m].x; f.jitter = a[m].jitter;
     f.Kc = a[m].Kc; f.D = a[m].D;
-    f.gran = a[m].gran; f.piv_off = f.T * f.T;
-    if ((a[m].cid != nullptr) != gather || a[m].tu || a[m].td || !f.gran)
+    f.gran = a[m].gran; f.piv_off = f.T * f.T; f.PB2 = a[m].PB2; f.epoch = a[m].epoch;
+    if ((a[m].cid != nullptr) != gather || a[m].tu || a[m].td || !f.gran || !f.PB2 || !f.epoch)
       return hipErrorInvalidValue;
     wmax = std::max(wmax, multi_workgroups(f.T));
   }

@@ -38,6 +38,7 @@ for k in range(16):
     NAMES[176 + k] = f"mc sweep {k}: V in LDS"
     NAMES[192 + k] = f"mc sweep {k}: pass-0 published"
     NAMES[208 + k] = f"mc sweep {k}: sweep done"
+    NAMES[224 + k] = f"mc sweep {k}: pass-0 products done"
 for k in range(16):
     NAMES[4 + k] = f"sweep {k} (pivot wg)"
     NAMES[20 + k] = f"  pivot in sweep {k}"
