@@ -724,139 +724,163 @@ constexpr int WT = 128;
 constexpr int WIDE_LDS = 2 * 2 * huge::KS * huge::S;  // the product loop's two staging buffers
 static_assert(WIDE_LDS >= PIVOT_LDS, "the pivot reuses the staging LDS");
 
-__global__ __launch_bounds__(256) void wide_update_kernel(BigSpdBatch b, int k, int skip_pivot, int gx,
-                                                          int per_xcd) {
+__global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int k, int skip_pivot, int gx,
+                                                          int per_xcd, int nx, int first) {
   using namespace huge;
-  // 1-D grid over both factors: blocks [0, nmat) are the factors' pivot workgroups (dispatched
-  // first: the pivot is the sweep's serial part); the tile workgroups after them are dealt
-  // XCD-major -- blocks t, t+8, ... share an XCD and get consecutive tiles, i.e. runs along block
-  // rows whose Z_I / Z_J panels stay in that XCD's L2.  gx = tiles per factor slot.
-  int m, x;
+  // 1-D grid over both factors.  8 nx PERSISTENT tile workgroups, two per CU, in two dispatch
+  // passes over the CUs: blocks [0, first) and [first + 8, first + 8 + (8 nx - first)); between
+  // them, blocks [first, first + 8) hold the factors' pivot workgroups (the sweep's serial part),
+  // in the first pass on CUs the second pass leaves alone (first = CUs - 8).  Tile workgroup t
+  // (its ordinal, = its block mod 8) works on XCD slot t & 7's run of per_xcd tiles (blocks t,
+  // t+8, ... share an XCD and take consecutive tiles, i.e. runs along block rows whose Z_I / Z_J
+  // panels stay in that XCD's L2), tile s + j nx of the run in round j.  A tile workgroup issues
+  // the next tile's first K-step loads before its current tile's stores (vector-memory
+  // operations complete in issue order): the stores drain under the next tile's product loop.
+  // gx = tiles per factor slot.
   __shared__ double sm[WIDE_LDS];
-  if ((int)blockIdx.x >= b.nmat + 8 * per_xcd) {  // the next sweep's panel (fused_panel)
+  const int L = blockIdx.x;
+  if (L >= 8 * nx + 8) {  // the next sweep's panel (fused_panel)
     const int tmax = max(b.T[0], b.nmat > 1 ? b.T[1] : 0);
-    const int pi = blockIdx.x - b.nmat - 8 * per_xcd;
-    m = pi / (2 * tmax);
+    const int pi = L - 8 * nx - 8;
+    const int m = pi / (2 * tmax);
     const int pj = pi % (2 * tmax);
+    if (m >= b.nmat) return;
     const int T2 = (b.p[m] + WT - 1) / WT;
-    if (m >= b.nmat || k + 1 >= T2 || skip_pivot || pj >= 2 * b.T[m]) return;
+    if (k + 1 >= T2 || skip_pivot || pj >= 2 * b.T[m]) return;
     fused_panel<2>(b, m, k, pj, (unsigned)(T2 - 1), sm);  // T2 - 1 panel-row tiles per sweep
     return;
   }
-  if ((int)blockIdx.x < b.nmat) {
-    m = blockIdx.x;
-    x = 0;
-  } else {
-    const int t = blockIdx.x - b.nmat;
-    const int wi = (t & 7) * per_xcd + (t >> 3);
-    if (wi >= b.nmat * gx) return;
-    m = wi / gx;
-    x = 1 + wi % gx;
-  }
-  const int p = b.p[m];
-  const int T2 = (p + WT - 1) / WT;  // 128-tiles per dimension
-  if (k >= T2) return;
-  const bool has_next = k + 1 < T2;
-  const bool LAST = !has_next;  // (per factor: the factors of a batch may differ in size)
-  const int nt = T2 * (T2 + 1) / 2;
-  const int Q = k + 1, qlin = Q * (Q + 1) / 2 + Q;
-  int ti, tj;
-  const bool pivot = x == 0;
-  if (pivot) {
-    if (!has_next || skip_pivot) return;
-    ti = tj = Q;
-  } else {
-    int lin = x - 1;
-    if (lin >= nt - (has_next ? 1 : 0)) return;
-    if (has_next && lin >= qlin) ++lin;  // (k+1, k+1) belongs to the pivot workgroup
-    tile_of(lin, ti, tj);
-  }
-  double* X = b.X[m];
-  const double* Z = zbuf<2>(b, m, k);
+  const bool pivot = L >= first && L < first + 8;
+  if (pivot && L - first >= b.nmat) return;
+  const int tt = L < first ? L : L - 8;  // tile workgroup ordinal
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  const int i0 = WT * ti, j0 = WT * tj;
-  const int wK = min(WT, p - WT * k);  // sweep width (a multiple of 32)
-  const bool inPi = ti == k, inPj = tj == k;
-  const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
-  // the tile's current values (zero base in the swept blocks; clamped addresses: rows / columns
-  // past p are never stored), held in registers (one wave per SIMD).  Vector-memory loads
-  // complete in issue order (vmcnt), so loading them up front held the first K-step's operands
-  // back behind 128 KB of HBM reads per tile: they are issued inside the product loop instead,
-  // one 16-row block at a time, each behind that K-step's operand fetch.
-  double xb[4][4][4];
-  const double f = (inPi || inPj) ? 0.0 : 1.0;
-  auto load_base = [&](int bx) {
-#pragma unroll
-    for (int by = 0; by < 4; ++by)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = min(i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r, p - 1);
-        const int col = min(j0 + 64 * wc + 16 * by + (lane & 15), p - 1);
-        xb[bx][by][r] = X[(size_t)row * p + col] * f;
-      }
+  // tile j of this workgroup -> (factor m, tile ti, tj); false past its run
+  auto tile_at = [&](int j, int& m, int& ti, int& tj) -> bool {
+    if (pivot) {
+      if (j > 0) return false;
+      m = L - first;
+      const int T2 = (b.p[m] + WT - 1) / WT;
+      if (k + 1 >= T2 || skip_pivot) return false;
+      ti = tj = k + 1;
+      return true;
+    }
+    const int loc = (tt >> 3) + j * nx;
+    if (loc >= per_xcd) return false;
+    const int wi = (tt & 7) * per_xcd + loc;
+    if (wi >= b.nmat * gx) return false;
+    m = wi / gx;
+    const int T2 = (b.p[m] + WT - 1) / WT;
+    if (k >= T2) return false;
+    const bool has_next = k + 1 < T2;
+    const int nt = T2 * (T2 + 1) / 2;
+    const int Q = k + 1, qlin = Q * (Q + 1) / 2 + Q;
+    int lin = wi % gx;
+    if (lin >= nt - (has_next ? 1 : 0)) return false;
+    if (has_next && lin >= qlin) ++lin;  // (k+1, k+1) belongs to the pivot workgroup
+    tile_of(lin, ti, tj);
+    return true;
   };
-  d4 acc[4][4];
-#pragma unroll
-  for (int bx = 0; bx < 4; ++bx)
-#pragma unroll
-    for (int by = 0; by < 4; ++by) acc[bx][by] = d4{0.0, 0.0, 0.0, 0.0};
-  // Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j]) -- gemm_huge_dev.h's
-  // product loop (product_t<1, 0>) with the base loads interleaved
-  {
-    constexpr int SZ = KS * S;
-    double* sA0 = sm;
-    double* sB0 = sm + 2 * SZ;
-    const int nk = wK / KS;
-    Regs R;
-    fetch<1, 0>(R, Z, p, Z, p, p, p, i0, j0, 0, t);
-    store<1, 0>(R, sA0, sB0, 1.0, t);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) fetch<1, 0>(R, Z, p, Z, p, p, p, i0, j0, (kt + 1) * KS, t);
+  constexpr int SZ = KS * S;
+  double* sA0 = sm;
+  double* sB0 = sm + 2 * SZ;
+  Regs R;
+  int m, ti, tj;
+  if (!tile_at(0, m, ti, tj)) return;
+  fetch<1, 0>(R, zbuf<2>(b, m, k), b.p[m], zbuf<2>(b, m, k), b.p[m], b.p[m], b.p[m], WT * ti, WT * tj, 0, t);
+  for (int j = 0;; ++j) {
+    const int p = b.p[m];
+    const int T2 = (p + WT - 1) / WT;  // 128-tiles per dimension
+    const bool has_next = k + 1 < T2;
+    const bool LAST = !has_next;  // (per factor: the factors of a batch may differ in size)
+    const int Q = k + 1;
+    double* X = b.X[m];
+    const double* Z = zbuf<2>(b, m, k);
+    const int i0 = WT * ti, j0 = WT * tj;
+    const int wK = min(WT, p - WT * k);  // sweep width (a multiple of 32)
+    const bool inPi = ti == k, inPj = tj == k;
+    const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
+    // the workgroup's next tile (its first K-step is fetched under this tile's last one)
+    int m2 = 0, ti2 = 0, tj2 = 0;
+    const bool more = tile_at(j + 1, m2, ti2, tj2);
+    // The accumulators start at the tile's current values (zero base in the swept blocks;
+    // clamped addresses: rows / columns past p are never stored) and the product is subtracted
+    // (A operand staged negated): no separate base registers.  The base loads are issued right
+    // behind the tile's first K-step operands (already in flight: fetched under the previous
+    // tile), so they overlap that K-step's staging; with two workgroups per CU the other one's
+    // MFMAs run under their HBM latency.
+    d4 acc[4][4];
+    {
+      const double f = (inPi || inPj) ? 0.0 : 1.0;
 #pragma unroll
       for (int bx = 0; bx < 4; ++bx)
-        if (kt == (bx * nk) / 4) load_base(bx);
-      mma(sA0 + cur * SZ, sB0 + cur * SZ, wr, wc, lane, acc);
-      if (kt + 1 < nk) store<1, 0>(R, sA0 + (cur ^ 1) * SZ, sB0 + (cur ^ 1) * SZ, 1.0, t);
-      __syncthreads();
+#pragma unroll
+        for (int by = 0; by < 4; ++by)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = min(i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r, p - 1);
+            const int col = min(j0 + 64 * wc + 16 * by + (lane & 15), p - 1);
+            acc[bx][by][r] = X[(size_t)row * p + col] * f;
+          }
     }
-  }
-  double mx = 0.0;
-#pragma unroll
-  for (int bx = 0; bx < 4; ++bx) {
-#pragma unroll
-    for (int by = 0; by < 4; ++by)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r;
-        const int col = j0 + 64 * wc + 16 * by + (lane & 15);
-        if (row < p && col < p) {
-          const double v = sgn * (xb[bx][by][r] - acc[bx][by][r]);
-          X[(size_t)row * p + col] = v;
-          if (LAST && row == col && row < b.n[m]) mx = fmax(mx, v);
+    // acc -= Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j]) -- gemm_huge_dev.h's
+    // product loop (product_t<1, 0>, A scaled by -1); R holds K-step 0's operands
+    {
+      const int nk = wK / KS;
+      store<1, 0>(R, sA0, sB0, -1.0, t);
+      __syncthreads();
+      for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) {
+          fetch<1, 0>(R, Z, p, Z, p, p, p, i0, j0, (kt + 1) * KS, t);
+        } else if (more) {
+          const double* Z2 = zbuf<2>(b, m2, k);
+          fetch<1, 0>(R, Z2, b.p[m2], Z2, b.p[m2], b.p[m2], b.p[m2], WT * ti2, WT * tj2, 0, t);
         }
+        mma(sA0 + cur * SZ, sB0 + cur * SZ, wr, wc, lane, acc);
+        if (kt + 1 < nk) store<1, 0>(R, sA0 + (cur ^ 1) * SZ, sB0 + (cur ^ 1) * SZ, -1.0, t);
+        __syncthreads();
       }
-    asm volatile("" ::: "memory");
-  }
-  if (LAST && ti == tj) {  // refinement gate: max_i (K^{-1})_ii
+    }
+    double mx = 0.0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-    if (lane == 0 && mx > 0.0)
-      atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
-                (unsigned long long)__double_as_longlong(mx));
-  }
-  if (!pivot) {
+    for (int bx = 0; bx < 4; ++bx) {
+#pragma unroll
+      for (int by = 0; by < 4; ++by)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r;
+          const int col = j0 + 64 * wc + 16 * by + (lane & 15);
+          if (row < p && col < p) {
+            const double v = sgn * acc[bx][by][r];
+            X[(size_t)row * p + col] = v;
+            if (LAST && row == col && row < b.n[m]) mx = fmax(mx, v);
+          }
+        }
+      asm volatile("" ::: "memory");
+    }
+    if (LAST && ti == tj) {  // refinement gate: max_i (K^{-1})_ii
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+      if (lane == 0 && mx > 0.0)
+        atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
+                  (unsigned long long)__double_as_longlong(mx));
+    }
+    if (pivot) {
+      // the next pivot block, factored in place from this workgroup's own stores (one L1 per
+      // workgroup: visible after the barrier)
+      __syncthreads();
+      const int r0 = WT * Q, w = min(WT, p - r0);
+      pivot128(X + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 4 * Q, b.status[m], sm);
+      release_add(b.flag[m] + 1, 1u);  // L^{-1} of pivot k + 1 ready (fused_panel)
+      return;
+    }
     if (has_next && (ti == Q || tj == Q)) release_add(b.flag[m] + 2, 1u);  // next panel row
-    return;
+    if (!more) return;
+    m = m2;
+    ti = ti2;
+    tj = tj2;
   }
-  // the next pivot block, factored in place from this workgroup's own stores (one L1 per
-  // workgroup: visible after the barrier)
-  __syncthreads();
-  const int r0 = WT * Q, w = min(WT, p - r0);
-  pivot128(X + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 4 * Q, b.status[m], sm);
-  release_add(b.flag[m] + 1, 1u);  // L^{-1} of pivot k + 1 ready (fused_panel)
 }
 
 // After the last 128-wide sweep: upper 64x64 tiles outside the diagonal 128 blocks <- the
@@ -898,6 +922,18 @@ BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   return b;
 }
 
+// CUs of the current device (the persistent update's workgroup count; 256 on a full MI355X)
+int wide_cus() {
+  static int cached = 0;
+  if (cached > 0) return cached;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return 256;
+  cached = cus;
+  return cached;
+}
+
 // workgroups of one 128-wide update launch: the pivot workgroup + one per lower 128-tile
 int wide_tiles(int Tmax) {
   const int T2 = (Tmax + 1) / 2;
@@ -917,8 +953,14 @@ void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int sta
   } else {
     const int k = stage >> 1, nsw = (Tmax + 1) / 2;
     const int gx = wide_tiles(Tmax) - 1, per_xcd = (nmat * gx + 7) / 8;
-    hipLaunchKernelGGL(wide_update_kernel, dim3(nmat + 8 * per_xcd + nmat * 2 * Tmax), dim3(256), 0, s, b, k,
-                       skip_pivot, gx, per_xcd);
+    // persistent tile workgroups: two per CU on all but the 8 CUs whose first-pass workgroup is a
+    // pivot slot (8 nx in all, nx per XCD slot), never more than the tiles
+    const int first = std::max(8, wide_cus() - 8);
+    const int nx = std::max(1, std::min(per_xcd, 2 * first / 8));
+    const int tile_wgs = 8 * nx;
+    const int fst = std::min(first, tile_wgs);  // (fewer tile workgroups than CUs: pivots right after)
+    hipLaunchKernelGGL(wide_update_kernel, dim3(tile_wgs + 8 + nmat * 2 * Tmax), dim3(256), 0, s, b, k,
+                       skip_pivot, gx, per_xcd, nx, fst);
     // after the last sweep of every factor (a smaller factor's last sweep came earlier; later
     // launches leave it alone)
     if (k + 1 == nsw)
