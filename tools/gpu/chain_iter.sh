@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_chain.py tests/test_gpu_chain_multi.py tests/test_gpu_fastgraph.py tests/test_gpu_dclass.py -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/pytest_chain.log 2>&1; rc=$?
+timeout -k 10 400 python -u -m pytest tests/test_gpu_chain.py tests/test_gpu_chain_multi.py tests/test_gpu_fastgraph.py tests/test_gpu_dclass.py tests/test_gpu_golden.py tests/test_gpu_dropin.py -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/pytest_chain.log 2>&1; rc=$?
 tail -3 gpurun_out/pytest_chain.log
 if [ $rc -ne 0 ]; then grep -E "^E |FAILED|Error|Timeout" gpurun_out/pytest_chain.log | head -30; exit 1; fi
 timeout -k 10 120 python tools/timeline.py --config C2 --steps 3 > gpurun_out/tl_c2.txt 2>&1 &&
