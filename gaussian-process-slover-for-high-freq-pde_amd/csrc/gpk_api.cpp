@@ -23,6 +23,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "../../include/gpk.h"
@@ -154,6 +155,10 @@ struct gpk_handle {
   // STEP_GRAPH_REPS training steps back to back in one graph ([0] fast, [1] full): one host
   // launch per group of steps (a graph launch boundary costs ~5-9 us of idle GPU)
   hipGraphExec_t g_multi[2] = {nullptr, nullptr};
+  // batch graphs of exactly `reps` steps ([0] fast, [1] full), captured by gpk_prepare for the
+  // chunk sizes a call of its step count runs (FAST_CHUNK and the remainder): a prepared call is
+  // one graph launch per chunk
+  std::map<int, hipGraphExec_t> g_batch[2];
   // one step(1) call as one graph ([0] fast, [1] full): batch begin (snapshot, counters), the
   // step, and the pinned-memory report -- the reference's one-call-per-iteration loop shape
   hipGraphExec_t g_call[2] = {nullptr, nullptr};
@@ -973,8 +978,9 @@ static int enqueue_step_shard(gpk_handle* h, int apply) {
 }
 
 constexpr int STEP_GRAPH_REPS = 8;
-static int capture(gpk_handle* h, int apply, bool refine = true, int reps = 1) {
-  hipGraphExec_t* slot = reps > 1 ? &h->g_multi[refine ? 1 : 0]
+static int capture(gpk_handle* h, int apply, bool refine = true, int reps = 1, bool batch = false) {
+  hipGraphExec_t* slot = batch ? &h->g_batch[refine ? 1 : 0][reps]
+                       : reps > 1 ? &h->g_multi[refine ? 1 : 0]
                                   : refine ? &h->g_exec[apply] : &h->g_fast[apply];
   if (*slot) return GPK_OK;
   if (h->shard && !h->comm->capturable())
@@ -1589,6 +1595,8 @@ int gpk_destroy(gpk_handle* h) {
     if (h->g_exec[k]) (void)hipGraphExecDestroy(h->g_exec[k]);
     if (h->g_fast[k]) (void)hipGraphExecDestroy(h->g_fast[k]);
     if (h->g_multi[k]) (void)hipGraphExecDestroy(h->g_multi[k]);
+    for (auto& kv : h->g_batch[k])
+      if (kv.second) (void)hipGraphExecDestroy(kv.second);
     if (h->g_call[k]) (void)hipGraphExecDestroy(h->g_call[k]);
   }
   for (int k = 0; k <= kMaxStages; ++k)
@@ -1691,6 +1699,18 @@ static int run_steps(gpk_handle* h, int n_steps, double* losses, bool fast, bool
     const int nb = std::min(LOSS_CAP, n_steps - done);
     if (reset_slot || done > 0) HIPCHK(hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s));
     int i = 0;
+    const auto& bg = h->g_batch[fast ? 0 : 1];
+    while (i < nb) {  // prepared batch graphs: the whole rest, else the largest that fits
+      auto it = bg.find(nb - i);
+      if (it == bg.end() || !it->second) {
+        it = bg.upper_bound(nb - i);
+        if (it == bg.begin()) break;
+        --it;
+        if (!it->second || it->first <= STEP_GRAPH_REPS) break;
+      }
+      HIPCHK(hipGraphLaunch(it->second, h->s));
+      i += it->first;
+    }
     if (multi)
       for (; i + STEP_GRAPH_REPS <= nb; i += STEP_GRAPH_REPS) HIPCHK(hipGraphLaunch(gm, h->s));
     for (; i < nb; ++i) HIPCHK(hipGraphLaunch(ge, h->s));
@@ -1709,6 +1729,7 @@ static int run_steps(gpk_handle* h, int n_steps, double* losses, bool fast, bool
 // open refinement gate costs a rerun of its chunk only (not of the whole call -- at C3 the
 // gate opens mid-training, and a 300-step call used to run twice).
 constexpr int FAST_CHUNK = 64;
+constexpr int kBatchMax = FAST_CHUNK;  // largest prepared batch graph
 
 int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
   if (!h) return fail(GPK_EINVAL, "NULL handle");
@@ -1782,6 +1803,13 @@ int gpk_prepare(gpk_handle* h, int32_t n_steps) {
     TRY(capture(h, 1, refine != 0));
     if (!h->shard) TRY(capture_call(h, refine == 0));
     if (!h->shard && n_steps >= STEP_GRAPH_REPS) TRY(capture(h, 1, refine != 0, STEP_GRAPH_REPS));
+    // the chunks of a call of n_steps (fast: FAST_CHUNK-step chunks + the remainder; the full
+    // graph runs them as one batch, decomposed the same way), one graph each
+    if (!h->shard && n_steps > STEP_GRAPH_REPS) {
+      const int full = std::min(n_steps, kBatchMax), rest = n_steps % kBatchMax;
+      TRY(capture(h, 1, refine != 0, full, true));
+      if (rest > STEP_GRAPH_REPS && rest != full) TRY(capture(h, 1, refine != 0, rest, true));
+    }
   }
   HIPCHK(hipStreamSynchronize(h->s));
   return GPK_OK;
