@@ -135,9 +135,14 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
 // grid.  The 4 waves take interleaved rows, load 4 rows' operands before accumulating (memory-
 // level parallelism), and keep V running sums per lane (one per distance variant of the lane's
 // diagonal, selected branch-free); they add them into LDS in wave order: deterministic.
-template <int V, int DERIV, bool MODE1D>
+// LDSB: the running sums as lane-private LDS bins instead (dynamic LDS [4 waves][2][vb][64]):
+// each pair is one ds_add_f64 per sum into its variant's bin -- O(1) per pair instead of the
+// V-way select (grids with many variants per diagonal, C2: 17).  A lane adds only into its own
+// bins, in program order, and the waves are added in the same fixed order: the same sums,
+// bitwise, as the register form.
+template <int V, int DERIV, bool MODE1D, bool LDSB = false>
 __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
-                                                       const StepScalars* __restrict__ sc) {
+                                                       const StepScalars* __restrict__ sc, int vb = 0) {
   const int axis = blockIdx.z, band = blockIdx.y, chunk = blockIdx.x;
   const PGradArgs& A = b.ax[axis];
   const ClassArgs& C = A.cls;
@@ -160,9 +165,17 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
     for (int o = 32; o > 0; o >>= 1) nvw = max(nvw, __shfl_xor(nvw, o, 64));
     nvw = __builtin_amdgcn_readfirstlane(nvw);
   }
-  double ak[V], ad[V];
+  double ak[LDSB ? 1 : V], ad[LDSB ? 1 : V];
 #pragma unroll
-  for (int x = 0; x < V; ++x) ak[x] = ad[x] = 0.0;
+  for (int x = 0; x < (LDSB ? 1 : V); ++x) ak[x] = ad[x] = 0.0;
+  extern __shared__ double lbin[];
+  double* mybin = lbin + (size_t)w * 2 * vb * 64;  // [2][vb][64] of this wave
+  if constexpr (LDSB) {
+    for (int x = 0; x < vb; ++x) {
+      mybin[x * 64 + lane] = 0.0;
+      mybin[(vb + x) * 64 + lane] = 0.0;
+    }
+  }
   double vs = 0.0, hc = 0.0;
   if (MODE1D) {
     vs = sc->v;
@@ -223,7 +236,16 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
       for (int s = 0; s < 8; ++s)
         if (!(xi[s] - xj[s] >= 0.0)) g1[s] = -g1[s];
     }
-    if constexpr (V > 16) {  // slot-major, bounded by the wave's variant count
+    if constexpr (LDSB) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int v = cv[s] - cb;
+        if (msk[s] && v >= 0 && v < vb) {
+          __hip_atomic_fetch_add(mybin + v * 64 + lane, g0[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(mybin + (vb + v) * 64 + lane, g1[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    } else if constexpr (V > 16) {  // slot-major, bounded by the wave's variant count
       int vv[8];
 #pragma unroll
       for (int s = 0; s < 8; ++s) vv[s] = ((cv[s] - cb) & msk[s]) | ~msk[s];
@@ -248,6 +270,26 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
         }
       }
     }
+  }
+  if constexpr (LDSB) {  // wave 0: the four waves' bins added in wave order, per variant
+    __syncthreads();
+    if (w == 0) {
+      double* pk = C.part + (size_t)chunk * C.ncls + cb;
+      double* pd = C.part + (size_t)(C.nchunk + chunk) * C.ncls + cb;
+      for (int x = 0; x < nvar; ++x) {
+        double rk = lbin[x * 64 + lane], rd = lbin[(vb + x) * 64 + lane];
+#pragma unroll
+        for (int ww = 1; ww < 4; ++ww) {
+          rk = rk + lbin[(size_t)ww * 2 * vb * 64 + x * 64 + lane];
+          rd = rd + lbin[(size_t)ww * 2 * vb * 64 + (vb + x) * 64 + lane];
+        }
+        pk[x] = rk;
+        pd[x] = rd;
+      }
+    }
+    if (TR_FIRST) TR_HI(SLOT_CLASS_SUM);
+    if (TR_LAST) TR_HI(SLOT_CSUM_START);
+    return;
   }
   __shared__ double red[2][V][64];
 #pragma unroll
@@ -471,6 +513,19 @@ static void launch_csum_v(const PGradBatch& b, int nchunk, int nbands, int deriv
     hipLaunchKernelGGL((class_sum_kernel<V, 1, false>), grid, dim3(256), 0, s, b, sc);
 }
 
+// many variants per diagonal (> 16): LDS bins sized to the variant count
+static void launch_csum_lds(const PGradBatch& b, int nchunk, int nbands, int deriv, int mode1d, int vmax,
+                            const StepScalars* sc, hipStream_t s) {
+  dim3 grid(nchunk, nbands, b.naxes);
+  const size_t lds = (size_t)4 * 2 * vmax * 64 * sizeof(double);
+  if (mode1d)
+    hipLaunchKernelGGL((class_sum_kernel<1, 2, true, true>), grid, dim3(256), lds, s, b, sc, vmax);
+  else if (deriv == 2)
+    hipLaunchKernelGGL((class_sum_kernel<1, 2, false, true>), grid, dim3(256), lds, s, b, sc, vmax);
+  else
+    hipLaunchKernelGGL((class_sum_kernel<1, 1, false, true>), grid, dim3(256), lds, s, b, sc, vmax);
+}
+
 template <bool MATERN, bool COS, bool CLS>
 static void launch_pg_c(const PGradBatch& b, int naxes, int bpa, int q, int deriv, int mode1d,
                         const StepScalars* sc, hipStream_t s) {
@@ -497,8 +552,7 @@ static void launch_pg_t(const PGradBatch& b, int naxes, int bpa, int q, int deri
       nchunk = std::max(nchunk, b.ax[k].cls.nchunk);
     }
     if (vmax <= 8) launch_csum_v<8>(b, nchunk, nbands, deriv, mode1d, sc, s);
-    else if (vmax <= 16) launch_csum_v<16>(b, nchunk, nbands, deriv, mode1d, sc, s);
-    else launch_csum_v<32>(b, nchunk, nbands, deriv, mode1d, sc, s);
+    else launch_csum_lds(b, nchunk, nbands, deriv, mode1d, vmax, sc, s);
     launch_pg_c<MATERN, COS, true>(b, naxes, bpa, q, deriv, mode1d, sc, s);
   } else {
     launch_pg_c<MATERN, COS, false>(b, naxes, bpa, q, deriv, mode1d, sc, s);
