@@ -186,10 +186,13 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
   // trip per pass.  Out-of-range pairs load the clamped element (0, 0) and get v = -1, which
   // matches no variant (bit-masked: a select on the loaded value let LLVM sink the load into an
   // exec-masked branch behind a vmcnt(0) wait).
-  for (int base = r0; base < r1; base += 16) {
-    int ii[8], jj[8], msk[8];
+  // (4 rows per wave and pass, 8 pairs; 8 rows -- twice the loads per round trip -- measured
+  // slower with the LDS bins: C2 30 -> 32 us, C4 3.5 -> 4.5 us)
+  constexpr int RP = 4, NP = 2 * RP;
+  for (int base = r0; base < r1; base += 4 * RP) {
+    int ii[NP], jj[NP], msk[NP];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < RP; ++s) {
       const int r = base + w + 4 * s;
       const bool in = kv && r < r1;
       const bool lo = in && r >= k, up = in && k > 0 && r + k < n;
@@ -200,14 +203,14 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
       jj[2 * s + 1] = up ? r + k : 0;
       msk[2 * s + 1] = -(int)up;
     }
-    int cv[8];
-    double g0[8], g1[8];
+    int cv[NP];
+    double g0[NP], g1[NP];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) cv[s] = C.cid[(size_t)ii[s] * p + jj[s]];
+    for (int s = 0; s < NP; ++s) cv[s] = C.cid[(size_t)ii[s] * p + jj[s]];
     if (MODE1D) {  // G_K = c/2 K^{-1} - 1/2 alpha alpha^T - v beta alpha^T, G_D = v R alpha^T
-      double ai[8], aj[8], bi[8], ri[8];
+      double ai[NP], aj[NP], bi[NP], ri[NP];
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < NP; ++s) {
         g0[s] = A.Kinv[(size_t)ii[s] * p + jj[s]];
         ai[s] = A.alpha[ii[s]];
         aj[s] = A.alpha[jj[s]];
@@ -215,30 +218,30 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
         ri[s] = A.R[ii[s]];
       }
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < NP; ++s) {
         g1[s] = vs * ri[s] * aj[s];
         g0[s] = hc * g0[s] - 0.5 * ai[s] * aj[s] - vs * bi[s] * aj[s];
       }
     } else {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) g0[s] = A.GK[(size_t)ii[s] * p + jj[s]];
+      for (int s = 0; s < NP; ++s) g0[s] = A.GK[(size_t)ii[s] * p + jj[s]];
 #pragma unroll
-      for (int s = 0; s < 8; ++s) g1[s] = A.GD[(size_t)ii[s] * p + jj[s]];
+      for (int s = 0; s < NP; ++s) g1[s] = A.GD[(size_t)ii[s] * p + jj[s]];
     }
     if (DERIV == 1) {
-      double xi[8], xj[8];
+      double xi[NP], xj[NP];
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < NP; ++s) {
         xi[s] = A.x[ii[s]];
         xj[s] = A.x[jj[s]];
       }
 #pragma unroll
-      for (int s = 0; s < 8; ++s)
+      for (int s = 0; s < NP; ++s)
         if (!(xi[s] - xj[s] >= 0.0)) g1[s] = -g1[s];
     }
     if constexpr (LDSB) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < NP; ++s) {
         const int v = cv[s] - cb;
         if (msk[s] && v >= 0 && v < vb) {
           __hip_atomic_fetch_add(mybin + v * 64 + lane, g0[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
