@@ -115,6 +115,27 @@ def test_multi_step_graph_bitwise_single(name):
     b.close()
 
 
+@pytest.mark.parametrize("name", ["2d_closed", "2d_open", "1d_closed"])
+def test_prepared_batch_graphs_bitwise_single(name):
+    """gpk_prepare(n) captures one graph per chunk size of a step(n) call (64 steps and the
+    remainder); prepared calls of 150 (64 + 64 + 22) and 22 steps, and an unprepared length
+    (falls back to 8-step + single-step graphs), are bitwise one graph launch per step --
+    fast batches (their chunk checks and rollbacks) included."""
+    prob, params, Q, fs = _case(name)
+    a = device_solver(prob, Q, fs)
+    b = device_solver(prob, Q, fs)
+    for s in (a, b):
+        s.set_params(params)
+    a.prepare(150)
+    la = np.concatenate([a.step(150), a.step(22), a.step(13)])
+    lb = np.concatenate([b.step(1) for _ in range(185)])
+    assert np.array_equal(la, lb)
+    for x, y in zip(_state(a), _state(b)):
+        assert np.array_equal(x, y)
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("name", ["2d_open", "1d_open"])
 def test_single_step_call_graph_rollback(name):
     """step(1) runs one captured call graph (batch begin + step + pinned-memory report); a fast
