@@ -40,3 +40,14 @@ def test_gpus_must_match_world_size():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.parametrize("config", ["C1", "C3"])
+def test_cpu_baseline_child_1d_and_2d(config):
+    """The bench's cpu_baseline leg (the oracle on the host, a child process) runs 1D and 2D
+    configs and reports a bounded sample: at least one full step, the thread counts used."""
+    sys.path.insert(0, ROOT)
+    import bench
+    r = bench.cpu_baseline_child(config, 0.2, 2)
+    assert r.get("value") and r["value"] > 0, r
+    assert r["cores"] == 2 and r["kind"] == "port" and config in r["sample"]
