@@ -159,6 +159,10 @@ struct gpk_handle {
   // chunk sizes a call of its step count runs (FAST_CHUNK and the remainder): a prepared call is
   // one graph launch per chunk
   std::map<int, hipGraphExec_t> g_batch[2];
+  // fast chunks of a prepared step(n) call as whole-call graphs: batch begin (the rollback
+  // snapshot) + `reps` steps + the pinned-memory report -- one launch and one synchronisation
+  // per chunk (capture_call's form for step(1))
+  std::map<int, hipGraphExec_t> g_calln;
   // one step(1) call as one graph ([0] fast, [1] full): batch begin (snapshot, counters), the
   // step, and the pinned-memory report -- the reference's one-call-per-iteration loop shape
   hipGraphExec_t g_call[2] = {nullptr, nullptr};
@@ -1040,6 +1044,39 @@ static int capture_call(gpk_handle* h, bool fast) {
   return GPK_OK;
 }
 
+// a fast chunk of `reps` steps as one graph: begin (snapshot, counters) + steps + report
+static int capture_calln(gpk_handle* h, int reps) {
+  hipGraphExec_t* slot = &h->g_calln[reps];
+  if (*slot) return GPK_OK;
+  const size_t np = (size_t)h->L.nparams;
+  hipGraph_t g = nullptr;
+  HIPCHK(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
+  StepBegin b{};
+  b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
+  b.snap_count = h->snap_count; b.count = h->count; b.viol = h->viol;
+  b.loss_slot = h->loss_slot;
+  int rc = check_launch(launch_step_begin(b, h->s), "step_begin");
+  for (int r = 0; r < reps && rc == GPK_OK; ++r) rc = enqueue_step(h, 1, false);
+  if (rc == GPK_OK) rc = check_launch(launch_step_report(make_report(h, true, reps), h->s), "step_report");
+  hipError_t e = hipStreamEndCapture(h->s, &g);
+  if (rc != GPK_OK) {
+    if (g) (void)hipGraphDestroy(g);
+    h->g_calln.erase(reps);
+    return rc;
+  }
+  if (e != hipSuccess) {
+    h->g_calln.erase(reps);
+    return fail(GPK_EHIP, std::string("capture: ") + hipGetErrorString(e));
+  }
+  e = hipGraphInstantiate(slot, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    h->g_calln.erase(reps);
+    return fail(GPK_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
+  }
+  return GPK_OK;
+}
+
 static int read_status(gpk_handle* h) {
   int st = 0;
   HIPCHK(hipMemcpyAsync(&st, h->status, sizeof(int), hipMemcpyDeviceToHost, h->s));
@@ -1597,6 +1634,9 @@ int gpk_destroy(gpk_handle* h) {
     if (h->g_multi[k]) (void)hipGraphExecDestroy(h->g_multi[k]);
     for (auto& kv : h->g_batch[k])
       if (kv.second) (void)hipGraphExecDestroy(kv.second);
+    if (k == 0)
+      for (auto& kv : h->g_calln)
+        if (kv.second) (void)hipGraphExecDestroy(kv.second);
     if (h->g_call[k]) (void)hipGraphExecDestroy(h->g_call[k]);
   }
   for (int k = 0; k <= kMaxStages; ++k)
@@ -1763,20 +1803,29 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
     const bool fast = h->fast_ok && h->fast_mode;
     const int n = fast ? std::min(FAST_CHUNK, n_steps - done) : n_steps - done;
     double* lo = losses ? losses + done : nullptr;
-    TRY(capture(h, 1, !fast));
-    {  // the snapshot of everything a fast batch carries forward (Up is rebuilt from params),
-       // the violation flag and the loss slot: one launch
-      StepBegin b{};
-      if (fast) {
-        b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
-        b.snap_count = h->snap_count; b.count = h->count; b.viol = h->viol;
-      }
-      b.loss_slot = h->loss_slot;
-      TRY(check_launch(launch_step_begin(b, h->s), "step_begin"));
-    }
-    TRY(run_steps(h, n, lo, fast, false));
     bool viol = false;
-    TRY(finish_batch(h, fast, &viol));
+    auto cg = fast && !h->shard ? h->g_calln.find(n) : h->g_calln.end();
+    if (cg != h->g_calln.end() && cg->second) {  // a prepared whole-chunk graph
+      HIPCHK(hipGraphLaunch(cg->second, h->s));
+      HIPCHK(hipStreamSynchronize(h->s));
+      h->pend_losses = lo;
+      h->pend_n = n;
+      TRY(read_report(h, true, &viol));
+    } else {
+      TRY(capture(h, 1, !fast));
+      {  // the snapshot of everything a fast batch carries forward (Up is rebuilt from params),
+         // the violation flag and the loss slot: one launch
+        StepBegin b{};
+        if (fast) {
+          b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
+          b.snap_count = h->snap_count; b.count = h->count; b.viol = h->viol;
+        }
+        b.loss_slot = h->loss_slot;
+        TRY(check_launch(launch_step_begin(b, h->s), "step_begin"));
+      }
+      TRY(run_steps(h, n, lo, fast, false));
+      TRY(finish_batch(h, fast, &viol));
+    }
     if (viol) {  // a step of the chunk needed refinement: roll back and rerun with the full graph
       ++h->rollbacks;
       HIPCHK(hipMemcpyAsync(h->params, h->snap, nb, hipMemcpyDeviceToDevice, h->s));
@@ -1809,6 +1858,12 @@ int gpk_prepare(gpk_handle* h, int32_t n_steps) {
       const int full = std::min(n_steps, kBatchMax), rest = n_steps % kBatchMax;
       TRY(capture(h, 1, refine != 0, full, true));
       if (rest > STEP_GRAPH_REPS && rest != full) TRY(capture(h, 1, refine != 0, rest, true));
+    }
+    // fast chunks as whole-call graphs (begin + steps + report)
+    if (!refine && !h->shard && n_steps > 1) {
+      const int full = std::min(n_steps, FAST_CHUNK), rest = n_steps % FAST_CHUNK;
+      TRY(capture_calln(h, full));
+      if (rest > 1 && rest != full) TRY(capture_calln(h, rest));
     }
   }
   HIPCHK(hipStreamSynchronize(h->s));
