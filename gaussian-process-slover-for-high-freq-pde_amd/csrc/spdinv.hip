@@ -492,6 +492,10 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
 
   for (int k = 0; k < T && !master; ++k) {
     const bool needI = I != k, needJ = J != k && J != I;
+    // issue priority over the CU's other workgroup when this tile feeds sweep k+1's panel or
+    // the pivot chain
+    if (I == k + 1 || (I == k + 2 && J == k + 2)) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
     // the panel tiles are usually published long before the pivot: fetch them first, then
     // wait for L^{-1}_k
     if (t == 0) {
@@ -804,6 +808,9 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
   for (int k = 0; k < T && !master; ++k) {
     // probes (gpk_trace.h SLOT_MC_*): the workgroup owning tile (k+2, k+2), factor 0
     const bool trc = t == 0 && m == 0 && hasdiag && k < 16 && (k + 2 == 2 * R || k + 2 == 2 * R + 1);
+    // issue priority: the sweep's front half (loads, V, the pass-0 tiles that feed sweep k+1 and
+    // the pivot chain) over the pass-1 products of the workgroup sharing this CU
+    __builtin_amdgcn_s_setprio(2);
     bool need[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -905,6 +912,7 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
       if (pass == 0 && trc) TR_HI(SLOT_MC_PROD + k);
       if (pass == 0 && k + 1 < T) publish_stores(k + 1);
       if (pass == 0 && trc) TR_HI(SLOT_MC_PUB + k);
+      if (pass == 0) __builtin_amdgcn_s_setprio(0);
     }
     {  // reset chunk k of this workgroup's share of the other half
       const size_t b0 = rs0 + (size_t)k * rchunk, b1 = std::min(rs1, b0 + rchunk);
