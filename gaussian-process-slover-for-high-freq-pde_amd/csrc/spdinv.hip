@@ -657,7 +657,7 @@ __host__ __device__ inline int multi_workgroups(int T) {  // per factor, + the p
 }
 
 template <int DERIV, bool GATHER>
-__global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
+__global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
   const int m = blockIdx.y;
   if (m == b.nmat) {
     if (blockIdx.x == 0) publish_prep(b.prep, b.q);
@@ -689,6 +689,7 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
   __shared__ double pool[32 * SA + 4 * 1024];
   __shared__ double pv[32];
   __shared__ unsigned int s_last;
+  __shared__ double sQ[4 * 16 * 17];  // per-wave transposition blocks (publish_stores)
   double* sL = pool;
   double* sV = pool + 32 * SA;
 
@@ -764,6 +765,22 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
     multi_slot(s, R, c0, I, J);
     return kk + 1 < T && I == kk + 1 && (J == kk || J == I);
   };
+  // a wave's 16x16 quadrant stored transposed -- element (row, col) of the tile to
+  // dst[col * ld + row] -- through its own LDS block (no workgroup barrier): each store
+  // instruction then writes 4 whole 128-B column segments instead of 16 lines x 32 B
+  auto put_transposed = [&](double* dst, size_t ld, const d4& a) {
+    double* q = sQ + wv * (16 * 17);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) q[((lane >> 4) + 4 * r) * 17 + (lane & 15)] = a[r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = lane + 64 * r, c = e >> 4, rr = e & 15;  // quadrant column c, row rr
+      st_sc1(dst + (size_t)(16 * wc + c) * ld + 16 * wr + rr, q[rr * 17 + c]);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
   // stores of every publishing tile (sc1, not waited for here)
   auto publish_stores = [&](int kk) {
 #pragma unroll
@@ -771,13 +788,14 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
       if (!valid(s) || !chain_in(s, kk)) continue;
       int I, J;
       multi_slot(s, R, c0, I, J);
+      if (I == J) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
-        if (I == J)
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
           st_sc1(gran_at(F, kk, 1, row * 32 + col), acc[s][r]);
-        else  // (kk+1, kk) -> element (col, row) of panel tile (kk, kk+1)
-          st_sc1(gran_at(F, kk, 0, col * 32 + row), acc[s][r]);
+        }
+      } else {  // (kk+1, kk) -> element (col, row) of panel tile (kk, kk+1)
+        put_transposed(gran_at(F, kk, 0, 0), 32, acc[s]);
       }
     }
 #pragma unroll
@@ -785,13 +803,14 @@ __global__ __launch_bounds__(256) void chain_multi_kernel(ChainBatch b) {
       if (!valid(s) || !publishes(s, kk)) continue;
       int I, J;
       multi_slot(s, R, c0, I, J);
+      if (I == kk) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
-        if (I == kk)
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * wr + (lane >> 4) + 4 * r, col = 16 * wc + (lane & 15);
           st_sc1(PBc + (size_t)(kk * 32 + row) * p + J * 32 + col, acc[s][r]);
-        else  // (I, kk) -> slot (kk, I) transposed
-          st_sc1(PBc + (size_t)(kk * 32 + col) * p + I * 32 + row, acc[s][r]);
+        }
+      } else {  // (I, kk) -> slot (kk, I) transposed
+        put_transposed(PBc + (size_t)(kk * 32) * p + I * 32, (size_t)p, acc[s]);
       }
     }
   };
