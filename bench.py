@@ -141,6 +141,7 @@ def large_factors(steps=3):
         inv_us = s.time_spd_inverse(3)
         n = 4096
         tus, tfl, _ = s.bench_kernel("spd_tiles", 3)
+        gus, _, gby = s.bench_kernel("gather", 5)
         path = s.inverse_path()
     finally:
         s.close()
@@ -148,8 +149,13 @@ def large_factors(steps=3):
     return {"config": "C5: advection 4096x4096, Matern52_Cos_1d, Q=30, fp64", "step_ms": step_ms,
             "inverse_path": path, "gemm_B_us": us, "gemm_tflops": gemm_tf,
             "gemm_mfma_frac": gemm_tf / PEAK_F64_TFLOPS, "spd_inverse_ms": inv_us / 1e3,
-            "cholesky_gflops": 2 * n ** 3 / (inv_us * 1e-6) / 1e9,
-            "spd_update_tflops": tfl / (tus * 1e-6) / 1e12}
+            "spd_inverse_gflops": 2 * n ** 3 / (inv_us * 1e-6) / 1e9,
+            "spd_update_tflops": tfl / (tus * 1e-6) / 1e12,
+            # K-assembly at size: gather_kernel writes K (+ its kept copy) and D of both 4096^2
+            # factors from the class values and reads each element's class id (bytes it moves)
+            "assembly": {"kernel": "gather_kernel (K, D [+ Kc] of both factors from class values)",
+                         "us": gus, "bytes": gby, "hbm_gbs": gby / (gus * 1e-6) / 1e9,
+                         "hbm_frac": gby / (gus * 1e-6) / 1e9 / PEAK_HBM_GBS}}
 
 
 def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
@@ -164,11 +170,14 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
         cid = key.split("_")[0]
         flags = GPK_FLAG_SPLIT_FACTORS if key.endswith("_split") else 0
         steps = a.sharded_steps if cid == "C4" else max(2, a.sharded_steps // 10)
+        STAGE["name"] = f"sharded {key}: create"
         s = shard.make_sharded_solver(cid, ctx, seed=0, flags=flags)
         try:
+            STAGE["name"] = f"sharded {key}: prepare + warm-up"
             s.prepare(steps)
             s.step(2)
             replicas.barrier(ctx)
+            STAGE["name"] = f"sharded {key}: {steps} timed steps"
             t0 = time.perf_counter()
             s.step(steps)
             t1 = time.perf_counter()
@@ -178,7 +187,28 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
         dt = replicas.max_over_ranks(t1 - t0, ctx)
         out[key] = {"value": steps / dt, "unit": "iters/s", "ms_per_step": dt / steps * 1e3,
                     "steps": steps, "ranks": ctx.world}
+    # C5 is reported both ways: both factors inverted on every rank, or one factor
+    # per rank half + a broadcast of K^{-1}; the default is the replicated form
+    out["C5_default"] = "C5 (replicated inverse); C5_split = GPK_FLAG_SPLIT_FACTORS"
     return out
+
+
+STAGE = {"name": "start"}   # what the sharded section is doing (reported when it fails)
+
+
+def dry_run_sharded_section(a, ctx):
+    """--dry-run --dry-run-sharded ok|hang|raise: a stand-in for sharded_section with the same
+    barrier / max-over-ranks plumbing; 'hang' blocks rank 1 (a stuck collective), 'raise' fails
+    rank 1.  Tests check that bench.py then exits non-zero."""
+    from gpk import replicas
+    STAGE["name"] = "dry-run sharded: timed steps"
+    if ctx.rank == 1 and a.dry_run_sharded == "hang":
+        time.sleep(3600)
+    if ctx.rank == 1 and a.dry_run_sharded == "raise":
+        raise RuntimeError("stand-in collective failed")
+    replicas.barrier(ctx)
+    dt = replicas.max_over_ranks(1e-3, ctx)
+    return {"dry-run": {"value": 1.0 / dt, "unit": "iters/s", "ranks": ctx.world}}
 
 
 def kernel_roofline(s, cfg, iters):
@@ -207,9 +237,16 @@ def kernel_roofline(s, cfg, iters):
     roof["avg_launch_us"] = d["us"]
     roof["alg_flops_per_launch"] = d["flops"]
     roof["alg_bytes_per_launch"] = d["bytes"]
-    # K-assembly HBM rate the north star asks for: K and D written per launch (16 n^2 B per
-    # axis) over the assembly launch's time (class values + gather when the chain gathers)
-    asm = kern.get("assemble")
+    # the step's assembly launch at this config, priced at the bytes it really moves: with the
+    # chain inverse that is the class-value launch (K and D at every distance class; the chain
+    # gathers K itself), a latency-bound launch whose GB/s is small by construction -- the
+    # HBM-bound K-assembly is measured at C5 size (large_factors.assembly)
+    a = kern.get("assemble")
+    asm = None
+    if a:
+        asm = {"kernel": "class_eval_kernel" if s.inverse_path() in ("chain", "chain_aug", "chain_multi")
+               else "assemble", "us": a["us"], "bytes": a["bytes"],
+               "hbm_gbs": a["bytes"] / (a["us"] * 1e-6) / 1e9}
     return roof, {k: round(v["us"], 3) for k, v in kern.items()}, asm
 
 
@@ -274,6 +311,8 @@ def main():
     ap.add_argument("--sharded-timeout", type=float, default=240.0)
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/rank plumbing only: gloo, stand-in solver, no GPU (tests)")
+    ap.add_argument("--dry-run-sharded", choices=["ok", "hang", "raise"], default=None,
+                    help=argparse.SUPPRESS)  # with --dry-run: a stand-in sharded section (tests)
     a = ap.parse_args()
     if a.cpu_baseline_only:
         print(json.dumps(cpu_baseline(a.config, a.cpu_seconds, a.cpu_threads, warmup=not a.cpu_no_warmup,
@@ -313,36 +352,49 @@ def main():
             s.step(1)
         extra["step1_per_call"] = {"value": a.step1_calls / (time.perf_counter() - t), "unit": "iters/s",
                                    "calls": a.step1_calls}
-        # fp64 SPD factor+inverse rate: potrf + potri = n^3 flops per Kronecker factor
+        # fp64 SPD inverse rate.  The path forms K^{-1} itself (Gauss-Jordan sweeps with Cholesky
+        # pivots: the log-det gradient needs c N/2 K^{-1}), so what is timed is potrf + potri
+        # together, priced at n^3 flops per Kronecker factor (potrf n^3/3 + potri 2n^3/3); there is
+        # no separate potrf launch to time alone
         inv_us = s.time_spd_inverse(20)
         n = cfg["n"]
         nfac = 2 if cfg["dim"] == 2 else 1
-        extra["cholesky_gflops"] = nfac * n ** 3 / (inv_us * 1e-6) / 1e9
+        extra["spd_inverse_gflops"] = nfac * n ** 3 / (inv_us * 1e-6) / 1e9
         extra["spd_inverse_us"] = inv_us
         roof, kus, asm = kernel_roofline(s, cfg, a.kernel_iters)
         extra["roofline"] = roof
         extra["kernels_us"] = kus
-        extra["assembly_hbm_gbs"] = asm["bytes"] / (asm["us"] * 1e-6) / 1e9 if asm else None
+        extra["assembly"] = asm
     final_loss = float(losses[-1])
     path = s.inverse_path()
     s.close()
 
-    if world > 1 and not a.dry_run and not a.no_sharded:
-        # strong scaling of ONE problem; a watchdog keeps a stuck collective from eating the line
+    failed = None
+    if world > 1 and (a.dry_run_sharded or (not a.dry_run and not a.no_sharded)):
+        # strong scaling of ONE problem.  A failure or a stuck collective is a FAILED run: the
+        # line is still printed (rank 0, the replicas' value + the error), the failing rank and
+        # stage go to stderr, and the process exits non-zero -- never a clean-looking rc 0.
         done = threading.Event()
         result = {}
 
         def watchdog():
             if not done.wait(a.sharded_timeout):
-                result["sharded"] = {"error": f"timeout after {a.sharded_timeout:.0f} s"}
+                msg = f"rank {rank}: timeout after {a.sharded_timeout:.0f} s in stage '{STAGE['name']}'"
+                print(f"bench.py: sharded section FAILED: {msg}", file=sys.stderr, flush=True)
                 if rank == 0:
+                    result["sharded"] = {"error": msg}
                     emit(a, value, dt, world, fast_graph, fast_end, rollbacks, final_loss, path, extra, result)
-                os._exit(0)
+                os._exit(3)   # (no re-exec, no cleanup: a collective may hold the GPU)
         threading.Thread(target=watchdog, daemon=True).start()
         try:
-            result["sharded"] = sharded_section(a, ctx)
-        except Exception as e:  # reported, never required
-            result["sharded"] = {"error": f"{type(e).__name__}: {e}"}
+            if a.dry_run_sharded:
+                result["sharded"] = dry_run_sharded_section(a, ctx)
+            else:
+                result["sharded"] = sharded_section(a, ctx)
+        except Exception as e:
+            failed = f"rank {rank}: {type(e).__name__}: {e} in stage '{STAGE['name']}'"
+            print(f"bench.py: sharded section FAILED: {failed}", file=sys.stderr, flush=True)
+            result["sharded"] = {"error": failed}
         done.set()
         extra.update(result)
 
@@ -358,6 +410,8 @@ def main():
 
     if rank == 0:
         emit(a, value, dt, world, fast_graph, fast_end, rollbacks, final_loss, path, extra)
+    if failed:
+        sys.exit(3)
     replicas.shutdown(ctx)
 
 
@@ -385,11 +439,13 @@ def emit(a, value, dt, world, fast_graph, fast_end, rollbacks, final_loss, path,
                    "equation": cfg["equation"],
                    "parallelism": f"replicas x{world} (one independent problem per GPU)"},
         "inverse_path": path,
-        "cholesky_gflops": extra.get("cholesky_gflops"),
+        "spd_inverse_gflops": extra.get("spd_inverse_gflops"),
+        "spd_inverse_flops": "n^3 per Kronecker factor = potrf n^3/3 + potri 2n^3/3 (K^{-1} formed, "
+                             "the log-det gradient needs it); the metric's 'Cholesky GFLOP/s'",
         "spd_inverse_us": extra.get("spd_inverse_us"),
         "roofline": extra.get("roofline"),
         "kernels_us": extra.get("kernels_us"),
-        "assembly_hbm_gbs": extra.get("assembly_hbm_gbs"),
+        "assembly": extra.get("assembly"),
         "step1_per_call": extra.get("step1_per_call"),
         "cpu_baseline": extra.get("cpu_baseline"),
         "cpu_baseline_1core": extra.get("cpu_baseline_1core"),

@@ -77,8 +77,7 @@ __device__ void pivot0(const AssembleArgs& A, unsigned need) {
   __shared__ double P[32 * SP], M[32 * SP], pv[32];
   const int t = threadIdx.x;
   if (t == 0) {
-    while (__hip_atomic_load(A.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
-      __builtin_amdgcn_s_sleep(1);
+    (void)spin_until_ge<1>(A.flag, need, A.status);  // bounded: status bit 2 on a lost hand-off
     *A.flag = 0u;  // re-arm for the next step (no other user until then)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // see the released tile rows
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -269,6 +268,24 @@ static void launch_class_t(const AssembleBatch& b, int naxes, int maxc, int maxt
     hipLaunchKernelGGL((class_eval_kernel<MATERN, COS, 0>), ge, dim3(256), 0, s, b, q);
     if (!eval_only) hipLaunchKernelGGL((gather_kernel<0>), gg, dim3(256), 0, s, b);
   }
+}
+
+// the gather launch alone (gpk_bench_kernel "gather": the K-assembly kernel's HBM rate); the
+// class values must be current (a class_eval launch ran since the parameters last changed)
+hipError_t launch_gather_only(const AssembleArgs* a, int naxes, hipStream_t s) {
+  AssembleBatch b{};
+  int maxtiles = 0;
+  for (int k = 0; k < naxes; ++k) {
+    b.ax[k] = a[k];
+    if (a[k].piv || a[k].cls.ncls <= 0) return hipErrorInvalidValue;
+    maxtiles = std::max(maxtiles, (a[k].p / 32) * (a[k].p / 32));
+  }
+  b.pivot_x = -1;
+  dim3 gg(naxes, maxtiles);
+  if (a[0].deriv == 2) hipLaunchKernelGGL((gather_kernel<2>), gg, dim3(256), 0, s, b);
+  else if (a[0].deriv == 1) hipLaunchKernelGGL((gather_kernel<1>), gg, dim3(256), 0, s, b);
+  else hipLaunchKernelGGL((gather_kernel<0>), gg, dim3(256), 0, s, b);
+  return hipGetLastError();
 }
 
 // rectangular block (preds' Kmn, gpk_kernel_matrices): no symmetry assumed

@@ -100,6 +100,7 @@ struct gpk_handle {
   StepScalars* sc = nullptr;
   int *count = nullptr, *loss_slot = nullptr, *status = nullptr;
   double *losses = nullptr, *diag = nullptr;
+  double* stat_x = nullptr;  // [2] status bits as doubles (split-factor group all-reduce)
 
   double *K[2] = {}, *Kb[2] = {}, *D[2] = {}, *Kinv[2] = {}, *piv[2] = {}, *ldet[2] = {};
   int nldet[2] = {0, 0};
@@ -535,16 +536,21 @@ static int build_descs(gpk_handle* h) {
     g.gate = h->pst[axis];
     return g;
   };
-  // Refinement GEMMs (X += K^{-1}(B - K X), gated on a cond(K) bound) run on the small-factor
-  // paths only.  On the large-factor 2D path they cost 6 of 19 N^3 GEMMs (C5: 22.7 of 64 ms)
-  // and buy nothing measurable: C5's dL/dU agrees with the LU oracle to 8.7e-8 without them
-  // vs 3.8e-8 with them, against a cond(K) budget of 2.4e-6 (tests/test_gpu_fullsize.py;
-  // numpy emulation of the blocked inverses: tools/solve_accuracy.py).  The 1D
-  // path keeps its refinement GEMVs: its kernel-parameter gradient is the sensitive one
-  // (C2: 3e-6 unrefined against 2.6e-7), and GEMVs cost microseconds.
-  const bool refine_stages = !h->bigspd;
+  // Refinement GEMMs (X += K^{-1}(B - K X)) are gated on device on a lower bound of cond(K): a
+  // closed gate ends each of their workgroups before any load (a launch).  Small factors: every
+  // solve is refined.  Large 2D factors (P >= 1600), where each refinement is two N^3 GEMMs
+  // (C5: ~2.2 ms each), by default the FORWARD solves A = K1^{-1} U and Bt = U K2^{-1}: the
+  // residual R = beta D1 A + Bt D2^T - F differentiates them (D amplifies the unstructured
+  // error of an explicit-inverse product) and ||R||^2 feeds the loss and the log_v gradient;
+  // GPK_FLAG_REFINE_ALL adds S and X1 / X2, GPK_FLAG_NO_REFINE drops all (round 2's path).
+  // Accuracy of each choice against the long-double yardstick: tests/test_gpu_accuracy.py,
+  // profiles/r3_parity.json, DESIGN.md §5.
+  const int rfl = h->prob.flags;
+  const bool ref_fwd = !h->bigspd || !(rfl & GPK_FLAG_NO_REFINE);
+  const bool ref_rev = !h->bigspd || ((rfl & GPK_FLAG_REFINE_ALL) && !(rfl & GPK_FLAG_NO_REFINE));
+  bool ref_now = ref_fwd;
   auto pushg = [&](const GemmDesc& g) {
-    if (refine_stages) d.push_back(g);
+    if (ref_now) d.push_back(g);
   };
   // X1 / X2 producers also write Y = S/2 + v X (GemmDesc::Y): G_K's left operand
   auto side = [&](GemmDesc g, double* Y) {
@@ -593,6 +599,7 @@ static int build_descs(gpk_handle* h) {
     d.push_back(r);
   }
   end(3);
+  ref_now = ref_rev;  // (the reverse-pass solves from here on)
   begin(4);  // W1 = A - S K2
   {
     GemmDesc g = mk(h->S, P2, 0, h->Kc[1], P2, 0, h->W1, P2, P1, P2, P2);
@@ -875,6 +882,12 @@ static int split_broadcast(gpk_handle* h) {
     TRY(h->comm->broadcast(h, h->ldet[b], (size_t)P / 32, root));
     TRY(h->comm->broadcast(h, h->pst[b], 2, root));
   }
+  // a non-PD factor (or a hand-off timeout) is seen on device by the ranks that inverted it
+  // only: sum the status bits over the group so that every rank returns GPK_ENOTPD -- a rank
+  // that carried on would enter the next step's collectives alone and hang
+  TRY(check_launch(launch_status_f64(h->status, h->stat_x, 0, h->s), "status_pack"));
+  TRY(h->comm->allreduce(h, h->stat_x, 2));
+  TRY(check_launch(launch_status_f64(h->status, h->stat_x, 1, h->s), "status_unpack"));
   return GPK_OK;
 }
 
@@ -923,15 +936,15 @@ static int build_shard(gpk_handle* h) {
   // rank contracts what it holds and the partials are all-reduced (enqueue_step_shard).
   auto g1 = [&](double* b) { return ShardGather{b, (size_t)h->h1 * P2}; };
   for (auto& v : h->sgather) v.clear();
-  const bool refine = h->st[1].n > 0;  // (2D large factors: no refinement stages)
-  if (refine) {
+  // (the refinement stages this handle has: build_descs, GPK_FLAG_REFINE_ALL / NO_REFINE)
+  if (h->st[1].n > 0) {
     h->sgather[0] = {g1(h->A)};                                // A_res: K1 A
     h->sgather[1] = {g1(h->W1)};                               // A_fix: K1^{-1} W1
   }
   h->sgather[2] = {g1(h->A)};                                  // R: D1 A;  G_K1 = Y1 A^T
   h->sgather[3] = {g1(h->R)};                                  // T1 = D1^T R
   h->sgather[6] = {g1(h->T1)};                                 // X1 = K1^{-1} T1
-  if (refine) {
+  if (h->st[8].n > 0) {
     h->sgather[7] = {g1(h->X1)};                               // D_res: K1 X1
     h->sgather[8] = {g1(h->W1)};                               // D_fix: K1^{-1} W1
   }
@@ -1077,12 +1090,33 @@ static int capture_calln(gpk_handle* h, int reps) {
   return GPK_OK;
 }
 
+// After a launch whose hand-off wait gave up (status bit 2), a late producer may still have
+// stored real words into hand-off slots the consumer had already consumed and reset: restore
+// every slot, flag and counter to its create-time state (the stream is synchronised, so every
+// launch has drained) before the handle is used again -- stale words would otherwise pass for
+// the next launch's inputs.
+static int reset_handoffs(gpk_handle* h) {
+  const Layout& L = h->L;
+  for (int a = 0; a < L.naxes; ++a) {
+    const size_t P = a == 0 ? L.p1 : L.p2, T = P / 32;
+    const size_t nflags = T * (T + (L.p1 + L.p2) / 32) + 2 * T + 1;
+    HIPCHK(hipMemsetD32Async(h->cgran[a], CHAIN_SENTINEL32, T * 4096, h->s));
+    if (h->PB2[a]) HIPCHK(hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * P * P, h->s));
+    if (h->cepoch[a]) HIPCHK(hipMemsetAsync(h->cepoch[a], 0, 4 * sizeof(unsigned int), h->s));
+    HIPCHK(hipMemsetAsync(h->cflags[a], 0, nflags * sizeof(unsigned int), h->s));
+    HIPCHK(hipMemsetAsync(h->aflag[a], 0, 4 * sizeof(unsigned int), h->s));
+  }
+  HIPCHK(hipStreamSynchronize(h->s));
+  return GPK_OK;
+}
+
 static int read_status(gpk_handle* h) {
   int st = 0;
   HIPCHK(hipMemcpyAsync(&st, h->status, sizeof(int), hipMemcpyDeviceToHost, h->s));
   HIPCHK(hipStreamSynchronize(h->s));
   if (st) {
     HIPCHK(hipMemsetAsync(h->status, 0, sizeof(int), h->s));
+    if (st & 2) TRY(reset_handoffs(h));
     return fail(GPK_ENOTPD, (st & 2) ? "SPD inverse: a pivot-chain hand-off timed out (device status 2)"
                                       : "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
   }
@@ -1117,6 +1151,7 @@ static int read_report(gpk_handle* h, bool fast, bool* violated) {
   *violated = false;
   if (st) {
     HIPCHK(hipMemsetAsync(h->status, 0, sizeof(int), h->s));
+    if (st & 2) TRY(reset_handoffs(h));
     return fail(GPK_ENOTPD, (st & 2) ? "SPD inverse: a pivot-chain hand-off timed out (device status 2)"
                                       : "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
   }
@@ -1364,6 +1399,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   A_(h->count, 1);
   A_(h->loss_slot, 1);
   A_(h->status, 1);
+  A_(h->stat_x, 2);
   A_(h->losses, LOSS_CAP);
   A_(h->diag, 8);
   for (int a = 0; a < L.naxes; ++a) {
@@ -1574,12 +1610,24 @@ static int group_run(gpk_handle** hs, int nranks, int apply, int n_steps) {
   for (auto& t : th) t.join();
   for (int r = 0; r < nranks; ++r)
     if (rcs[r] != GPK_OK) return fail(rcs[r], "rank " + std::to_string(r) + ": " + errs[r]);
-  int rc = GPK_OK;
-  for (int r = 0; r < nranks && rc == GPK_OK; ++r) {
+  // every rank's status: a group whose ranks disagree (some report a non-PD factor, some not)
+  // would, under RCCL, leave the reporting ranks out of the next step's collectives -- the step
+  // makes the status group-wide (split_broadcast); a disagreement here is an internal error
+  int rc = GPK_OK, bad = 0;
+  std::string first;
+  for (int r = 0; r < nranks; ++r) {
     DevSwitch ds(hs[r]->dev);
-    rc = read_status(hs[r]);
+    const int rr = read_status(hs[r]);
+    if (rr != GPK_OK) {
+      if (!bad++) first = g_err;
+      rc = rr;
+    }
   }
-  return rc;
+  if (bad && bad != nranks)
+    return fail(GPK_EINVAL, "internal: device status differs across the ranks of the group (" +
+                                std::to_string(bad) + " of " + std::to_string(nranks) + "): " + first);
+  if (rc != GPK_OK) return fail(rc, first);
+  return GPK_OK;
 }
 
 int gpk_group_step(gpk_handle** hs, int32_t nranks, int32_t n_steps, double* losses) {
@@ -2003,12 +2051,17 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
     gv(Kmn1, alpha, res, m1, 1.0, nullptr, 0.0);  // preds = Kmn K^{-1} u
     (void)hipMemcpyAsync(out, res, m1 * sizeof(double), hipMemcpyDeviceToHost, h->s);
   } else {
-    // U_pred = Kmn1 (K1^{-1} U K2^{-1}) Kmn2^T   (model_GP_solver_2d.py:185-220)
+    // U_pred = Kmn2 (K2^{-1} (Kmn1 K1^{-1} U)^T), associated exactly as the reference does
+    // (model_GP_solver_2d.py:185-220: M1 = Kmn K1inv_U, M2 = solve(K2, M1^T), Kmn2 M2): every
+    // intermediate stays O(|U_pred|) after its Kmn product.  (Forming S = K1^{-1} U K2^{-1}
+    // first, as rounds 1-2 did, builds entries ~ |U| / jitter^2 whose cancellation in
+    // Kmn1 S Kmn2^T cost up to 0.37 relative L2 at C5 with a random field.)
     const int M2p = pad_up(m2), P2 = L.p2;
-    double *dx2, *Kmn2, *Aw, *Sw, *Mw, *Rw;
+    double *dx2, *Kmn2, *Aw, *Rw, *Mw, *Nw, *Rm;
     if ((r = dalloc(&dx2, m2)) || (r = dalloc(&Kmn2, (size_t)M2p * P2)) || (r = dalloc(&Aw, (size_t)P1 * P2)) ||
-        (r = dalloc(&Sw, (size_t)P1 * P2)) || (r = dalloc(&Mw, (size_t)M1p * P2)) ||
-        (r = dalloc(&Rw, (size_t)P1 * P2)) || (r = dalloc(&res, (size_t)M1p * M2p))) { cleanup(); return r; }
+        (r = dalloc(&Rw, (size_t)P1 * P2)) || (r = dalloc(&Mw, (size_t)M1p * P2)) ||
+        (r = dalloc(&Nw, (size_t)M1p * P2)) || (r = dalloc(&Rm, (size_t)M1p * P2)) ||
+        (r = dalloc(&res, (size_t)M1p * M2p))) { cleanup(); return r; }
     (void)hipMemcpyAsync(dx2, xte2, m2 * sizeof(double), hipMemcpyHostToDevice, h->s);
     (void)launch_cross(h->prob.kind, L.q, dx2, m2, h->x2, L.n2, P2, h->kc + 1, 0.0, 0, Kmn2, nullptr, h->s);
     GemmDesc d[8] = {};
@@ -2017,19 +2070,19 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
       g.A = A; g.lda = lda; g.ta = ta; g.B = B; g.ldb = ldb; g.tb = tb; g.C = C; g.ldc = ldc;
       g.M = M; g.N = N; g.K = K; g.alpha = 1.0; g.epi = EPI_STORE;
     };
-    // A = K1^{-1} U and S = A K2^{-1}, each with one refinement step (solve() accuracy)
+    // A = K1^{-1} U and N = M1 K2^{-1}, each with one refinement step (solve() accuracy)
     mk(d[0], h->Kinv[0], P1, 0, h->Up, P2, 0, Aw, P2, P1, P2, P1);
     mk(d[1], h->Kc[0], P1, 0, Aw, P2, 0, Rw, P2, P1, P2, P1);          // Rw = U - K1 A
     d[1].alpha = -1.0; d[1].beta = 1.0; d[1].C0 = h->Up; d[1].ldc0 = P2;
     mk(d[2], h->Kinv[0], P1, 0, Rw, P2, 0, Aw, P2, P1, P2, P1);        // A += K1^{-1} Rw
     d[2].beta = 1.0; d[2].C0 = Aw; d[2].ldc0 = P2;
-    mk(d[3], Aw, P2, 0, h->Kinv[1], P2, 0, Sw, P2, P1, P2, P2);
-    mk(d[4], Sw, P2, 0, h->Kc[1], P2, 0, Rw, P2, P1, P2, P2);          // Rw = A - S K2
-    d[4].alpha = -1.0; d[4].beta = 1.0; d[4].C0 = Aw; d[4].ldc0 = P2;
-    mk(d[5], Rw, P2, 0, h->Kinv[1], P2, 0, Sw, P2, P1, P2, P2);        // S += Rw K2^{-1}
-    d[5].beta = 1.0; d[5].C0 = Sw; d[5].ldc0 = P2;
-    mk(d[6], Kmn1, P1, 0, Sw, P2, 0, Mw, P2, M1p, P2, P1);
-    mk(d[7], Mw, P2, 0, Kmn2, P2, 1, res, M2p, M1p, M2p, P2);
+    mk(d[3], Kmn1, P1, 0, Aw, P2, 0, Mw, P2, M1p, P2, P1);             // M1 = Kmn1 A
+    mk(d[4], Mw, P2, 0, h->Kinv[1], P2, 0, Nw, P2, M1p, P2, P2);       // N = M1 K2^{-1} = M2^T
+    mk(d[5], Nw, P2, 0, h->Kc[1], P2, 0, Rm, P2, M1p, P2, P2);         // Rm = M1 - N K2
+    d[5].alpha = -1.0; d[5].beta = 1.0; d[5].C0 = Mw; d[5].ldc0 = P2;
+    mk(d[6], Rm, P2, 0, h->Kinv[1], P2, 0, Nw, P2, M1p, P2, P2);       // N += Rm K2^{-1}
+    d[6].beta = 1.0; d[6].C0 = Nw; d[6].ldc0 = P2;
+    mk(d[7], Nw, P2, 0, Kmn2, P2, 1, res, M2p, M1p, M2p, P2);       // U_pred = N Kmn2^T
     const int force_big = gemm_force(h->prob.flags);
     for (int k = 0; k < 8; ++k)
       (void)launch_gemm_auto(d + k, 1, h->sc, h->s, gemm_variant(d + k, 1, force_big));
@@ -2339,6 +2392,32 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
       flops += n * n * n / ((a == 0 ? L.p1 : L.p2) / 32);
       bytes += 16.0 * n * n;
     }
+  } else if (nm == "gather") {
+    // the K-assembly launch of the class path (the large-factor step's, gpk_api.cpp
+    // enqueue_assemble_inverse): K (+ jitter), its kept copy Kc (when the handle keeps one) and D
+    // written, the int32 class id of every element read -- the bytes it really moves; the class
+    // values (U doubles per field) are L2-resident gathers and not counted
+    if (h->cls[0].ncls <= 0) return fail(GPK_EINVAL, "gather: this handle does not use distance classes");
+    for (int a = 0; a < L.naxes; ++a) {
+      aa[a].cls = h->cls[a];
+      aa[a].Kc = h->Kc[a];
+    }
+    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s, true),
+                     "class_eval"));
+    launch = [&]() { return launch_gather_only(aa, L.naxes, h->s); };
+    for (int a = 0; a < L.naxes; ++a) {
+      const double P = a == 0 ? L.p1 : L.p2;
+      bytes += P * P * (4.0 + 8.0 + (h->Kc[a] ? 8.0 : 0.0) + (deriv ? 8.0 : 0.0));
+    }
+  } else if (nm == "class_eval") {
+    // the class-value launch (every field at every class distance + the step constants): it
+    // reads the U class distances and writes K and D values per class (24 B per class and axis)
+    if (h->cls[0].ncls <= 0) return fail(GPK_EINVAL, "class_eval: this handle does not use distance classes");
+    for (int a = 0; a < L.naxes; ++a) aa[a].cls = h->cls[a];
+    launch = [&]() {
+      return launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s, true);
+    };
+    for (int a = 0; a < L.naxes; ++a) bytes += 24.0 * h->cls[a].ncls;
   } else if (nm == "assemble") {
     // the step's assembly launch(es): class values only when the chain gathers K itself
     const bool eval_only = h->chain && h->cls[0].ncls > 0;
@@ -2346,8 +2425,13 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     launch = [&, eval_only]() {
       return launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s, eval_only);
     };
-    // K and D written (8 B each per element); flops not counted (transcendental-bound)
-    for (int a = 0; a < L.naxes; ++a) { const double n = a == 0 ? n1 : n2; bytes += 16.0 * n * n; }
+    // the bytes the launch really moves: with classes and the chain, the class values (24 B per
+    // class: distance read, K and D value written); otherwise K and D written per element (P^2
+    // per axis, 8 B each); flops not counted (transcendental-bound)
+    for (int a = 0; a < L.naxes; ++a) {
+      const double P = a == 0 ? L.p1 : L.p2;
+      bytes += eval_only ? 24.0 * h->cls[a].ncls : 16.0 * P * P;
+    }
   } else if (nm == "gemm_B" && L.dim == 2) {
     launch = [&]() {
       return launch_gemm_auto(h->hdescs.data() + h->st[3].off, h->st[3].n, h->sc, h->s, h->st[3].variant);

@@ -143,6 +143,8 @@ struct AssembleArgs {
   unsigned int* flag;    // zero-initialised counter (re-armed by the pivot workgroup)
   ClassArgs cls;         // ncls > 0: class evaluation + gather instead of per-pair evaluation
 };
+// the class path's gather launch alone (K, Kc, D from current class values; no pivot 0)
+hipError_t launch_gather_only(const AssembleArgs* a, int naxes, hipStream_t s);
 // eval_only (class path): the class values (+ prep) only, no gather / pivot-0 launch
 hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, const PrepArgs& prep,
                            hipStream_t s, bool eval_only = false);

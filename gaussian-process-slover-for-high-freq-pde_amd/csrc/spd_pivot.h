@@ -8,6 +8,26 @@ namespace gpk {
 constexpr int SP = 33;  // pivot scratch stride
 typedef __attribute__((address_space(3))) double* lds_ptr;
 
+// Every inter-workgroup wait of the persistent / flag-ordered kernels is bounded: 2^22 polls
+// (seconds, far beyond any hand-off of a running step) and the wait gives up, setting status
+// bit 2 -- the step then reports GPK_ENOTPD ("hand-off timed out") instead of hanging the device
+// (a producer that is not resident, e.g. another process holding the CUs).  The host resets the
+// hand-off slots after such a launch (gpk_api.cpp reset_handoffs).
+constexpr unsigned SPIN_CAP = 1u << 22;
+template <int SLEEP = 1>
+__device__ __forceinline__ bool spin_until_ge(const unsigned int* c, unsigned int target, int* status) {
+  for (unsigned spins = 0;
+       __hip_atomic_load(const_cast<unsigned int*>(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
+       ++spins) {
+    if (spins == SPIN_CAP) {
+      atomicOr(status, 2);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(SLEEP);
+  }
+  return true;
+}
+
 // v_rsq_f64 is 2^-24.2 relative (tools/probes/rsq_probe.hip): one Newton step leaves 4e-15,
 // two 1.4e-16.  One third-order step y (1 + e/2 + 3e^2/8), e = 1 - p y^2 (truncation ~e^3/3 =
 // 2^-70) reaches the same accuracy in 4 dependent operations after the rsq instead of 6: the

@@ -247,9 +247,9 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 __device__ __forceinline__ double ld_sc1(const double* p) {
   return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void wait_flag(unsigned int* f) {
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    __builtin_amdgcn_s_sleep(1);
+// bounded (spd_pivot.h spin_until_ge): a flag that never rises sets status bit 2
+__device__ __forceinline__ void wait_flag(unsigned int* f, int* status) {
+  (void)spin_until_ge<1>(f, 1u, status);
 }
 // every wave drained its sc1 stores -> barrier -> one lane raises the flag
 __device__ __forceinline__ void signal_flag(unsigned int* f) {
@@ -499,8 +499,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
     // the panel tiles are usually published long before the pivot: fetch them first, then
     // wait for L^{-1}_k
     if (t == 0) {
-      if (needI) wait_flag(panel_rdy + k * TC + I);
-      if (needJ) wait_flag(panel_rdy + k * TC + J);
+      if (needI) wait_flag(panel_rdy + k * TC + I, F.status);
+      if (needJ) wait_flag(panel_rdy + k * TC + J, F.status);
     }
     __syncthreads();
     double xi[4], xj[4];
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
       xi[r] = needI ? ld_sc1(F.PB + (size_t)(k * 32 + row) * p + I * 32 + tx) : 0.0;
       xj[r] = needJ ? ld_sc1(panel_ptr(k, row, tx)) : 0.0;
     }
-    if (t == 0) wait_flag(piv_rdy + k);
+    if (t == 0) wait_flag(piv_rdy + k, F.status);
     __syncthreads();
     const bool trl = t == 0 && m == 0 && k == T - 1 && I == T - 1 && J == T - 1;
     if (trl) TR_HI(SLOT_LAST_FLAG);
@@ -865,7 +865,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
       load_panel();
     }
     if (trc) TR_HI(SLOT_MC_PANEL + k);
-    if (t == 0) wait_flag(piv_rdy + k);
+    if (t == 0) wait_flag(piv_rdy + k, F.status);
     if (trc) TR_HI(SLOT_MC_PIV + k);
     __syncthreads();
     const double* Li = F.piv + (size_t)k * 1024;

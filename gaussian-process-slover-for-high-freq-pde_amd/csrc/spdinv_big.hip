@@ -304,10 +304,9 @@ __device__ __forceinline__ void release_add(unsigned int* c, unsigned int v) {
     atomicAdd(c, v);
   }
 }
-__device__ __forceinline__ void acquire_wait(const unsigned int* c, unsigned int target) {
+__device__ __forceinline__ void acquire_wait(const unsigned int* c, unsigned int target, int* status) {
   if (threadIdx.x == 0) {
-    while (__hip_atomic_load(const_cast<unsigned int*>(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
-      __builtin_amdgcn_s_sleep(2);
+    (void)spin_until_ge<2>(c, target, status);  // bounded: status bit 2 on a lost hand-off
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
@@ -416,8 +415,8 @@ __global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
 template <int R>
 __device__ void fused_panel(const BigSpdBatch& b, int m, int k, int pj, unsigned int row_tiles, double* sm) {
   const unsigned int* fl = b.flag[m];
-  acquire_wait(fl + 1, (unsigned)(k + 1));
-  acquire_wait(fl + 2, (unsigned)(k + 1) * row_tiles);
+  acquire_wait(fl + 1, (unsigned)(k + 1), b.status[m]);
+  acquire_wait(fl + 2, (unsigned)(k + 1) * row_tiles, b.status[m]);
   panel_block<R>(b, m, k + 1, pj / R, pj % R, sm);
 }
 
@@ -522,8 +521,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (x == 1) {
     if (!has_next || skip_pivot) return;
     if (threadIdx.x == 0) {  // pivot workgroup for block k+1
-      while (__hip_atomic_load(b.flag[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)tl.nh)
-        __builtin_amdgcn_s_sleep(2);
+      (void)spin_until_ge<2>(b.flag[m], (unsigned)tl.nh, b.status[m]);  // bounded (status bit 2)
       *b.flag[m] = 0u;  // re-arm (next user: the next sweep's update launch)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -98,5 +98,6 @@ hipError_t launch_adam_u(const AdamUArgs& a, hipStream_t s);
 hipError_t launch_sync_u(const double* params, const Layout& L, double* Up, hipStream_t s);
 hipError_t launch_params_from_up(const double* Up, const Layout& L, double* params, hipStream_t s);
 hipError_t launch_add_into(double* dst, const double* src, size_t n, hipStream_t s);
+hipError_t launch_status_f64(int* st, double* x, int mode, hipStream_t s);
 
 }  // namespace gpk

@@ -131,6 +131,25 @@ hipError_t launch_add_into(double* dst, const double* src, size_t n, hipStream_t
   return hipGetLastError();
 }
 
+// Status word <-> two doubles (bit 1: non-positive pivot, bit 2: hand-off timeout), so that a
+// summing all-reduce makes the status of a split-factor rank group group-wide (gpk_api.cpp
+// split_broadcast): mode 0 packs, mode 1 ORs the summed bits back into the word.
+__global__ void status_f64_kernel(int* st, double* x, int mode) {
+  if (threadIdx.x != 0) return;
+  if (mode == 0) {
+    const int v = *st;
+    x[0] = (v & 1) ? 1.0 : 0.0;
+    x[1] = (v & 2) ? 1.0 : 0.0;
+  } else {
+    *st |= (x[0] > 0.0 ? 1 : 0) | (x[1] > 0.0 ? 2 : 0);
+  }
+}
+
+hipError_t launch_status_f64(int* st, double* x, int mode, hipStream_t s) {
+  hipLaunchKernelGGL(status_f64_kernel, dim3(1), dim3(64), 0, s, st, x, mode);
+  return hipGetLastError();
+}
+
 // Start of a gpk_step batch, one launch instead of five copies / memsets: the rollback snapshot
 // of params, m, v and the Adam count (snap != nullptr), the refinement-violation flag and the
 // loss-ring slot zeroed.

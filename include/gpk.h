@@ -115,6 +115,11 @@ typedef struct gpk_problem {
  * 64-row macro tiles of the lower triangle, when its grid is co-resident (p <= 2048 on a full
  * MI355X); GPK_FLAG_NO_CHAIN or GPK_FLAG_FORCE_BIG_SPD select the launch-per-sweep path. */
 #define GPK_FLAG_FORCE_CHAIN_MULTI 4096 /* the macro-tile chain at every 1D size (tests) */
+/* Large 2D factors (P >= 1600): which solves get one (cond-gated) refinement step.  Default: the
+ * forward solves A = K1^{-1} U, Bt = U K2^{-1}; REFINE_ALL: also S and X1 / X2 (every solve, as
+ * the small-factor path); NO_REFINE: none (explicit-inverse products only). */
+#define GPK_FLAG_REFINE_ALL 8192
+#define GPK_FLAG_NO_REFINE 16384
 
 typedef struct gpk_handle gpk_handle;
 

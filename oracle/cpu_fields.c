@@ -184,14 +184,17 @@ void oracle_param_grad(int kind, int deriv, const double* x, int n, const double
     a[q] = exp(logls[q]);
   }
   memset(out, 0, sizeof(double) * 3 * Q);
+  /* per-row partials, summed in row order afterwards: the result does not depend on the thread
+   * count or the dynamic schedule (the GPU comparisons need a reproducible oracle) */
+  double* rowp = (double*)calloc((size_t)n * 3 * Q, sizeof(double));
 #pragma omp parallel
   {
-    double* acc = (double*)calloc(3 * Q, sizeof(double));
     double* wk = (double*)malloc(sizeof(double) * n);
     double* wd = (double*)malloc(sizeof(double) * n);
     double* dd = (double*)malloc(sizeof(double) * n);
 #pragma omp for schedule(dynamic, 8)
     for (int i = 0; i < n; ++i) {
+      double* acc = rowp + (size_t)i * 3 * Q;
       /* weights of the unordered pairs (i, j), j <= i */
       for (int j = 0; j <= i; ++j) {
         const double diff = x[i] - x[j];
@@ -218,18 +221,18 @@ void oracle_param_grad(int kind, int deriv, const double* x, int n, const double
           else if (deriv == 1) pg_row_t(0, 1, i + 1, dd, wk, wd, aq, om, &sf, &sl, &sw);
           else pg_row_t(0, 0, i + 1, dd, wk, wd, aq, om, &sf, &sl, &sw);
         }
-        acc[q] += sf;
-        acc[Q + q] += sl;
-        acc[2 * Q + q] += sw;
+        acc[q] = sf;
+        acc[Q + q] = sl;
+        acc[2 * Q + q] = sw;
       }
     }
-#pragma omp critical
-    for (int t = 0; t < 3 * Q; ++t) out[t] += acc[t];
-    free(acc);
     free(wk);
     free(wd);
     free(dd);
   }
+  for (int i = 0; i < n; ++i)
+    for (int t = 0; t < 3 * Q; ++t) out[t] += rowp[(size_t)i * 3 * Q + t];
+  free(rowp);
   for (int q = 0; q < Q; ++q) {
     out[q] *= w[q];
     out[Q + q] *= w[q];

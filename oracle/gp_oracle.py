@@ -274,7 +274,31 @@ def set_extended(flag):
     _EXTENDED = bool(flag)
 
 
-def _ext_lu(K):
+_EXTLIB = None
+
+
+def _extlib():
+    """oracle/ext_solve.c (blocked, OpenMP long-double LU + solves), or None if not built."""
+    global _EXTLIB
+    if _EXTLIB is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libgpk_ext.so")
+        if not os.path.exists(path) or np.dtype(np.longdouble).itemsize != 16:
+            _EXTLIB = False
+            return None
+        lib = ctypes.CDLL(path)
+        vp, i = ctypes.c_void_p, ctypes.c_int
+        lib.ld_lu.argtypes = [i, vp, vp]
+        lib.ld_lu.restype = i
+        lib.ld_lu_solve.argtypes = [i, vp, vp, i, vp, vp]
+        lib.ld_lu_logabsdet.argtypes = [i, vp]
+        lib.ld_lu_logabsdet.restype = ctypes.c_double
+        _EXTLIB = lib
+    return _EXTLIB or None
+
+
+def _ext_lu_py(K):
     A = np.array(K, dtype=np.longdouble)
     n = A.shape[0]
     perm = np.arange(n)
@@ -288,7 +312,7 @@ def _ext_lu(K):
     return A, perm
 
 
-def _ext_solve(f, B):
+def _ext_solve_py(f, B):
     A, perm = f
     n = A.shape[0]
     X = np.array(B, dtype=np.longdouble)[perm]
@@ -298,6 +322,32 @@ def _ext_solve(f, B):
         X[k] /= A[k, k]
         X[:k] -= np.multiply.outer(A[:k, k], X[k])
     return X.astype(np.float64)
+
+
+def _ext_lu(K):
+    """Long-double LU with partial pivoting (getrf in 80-bit): the C kernel when built, else
+    the NumPy loops (same algorithm, same pivots)."""
+    lib = _extlib()
+    if lib is None:
+        return _ext_lu_py(K)
+    A = np.array(K, dtype=np.longdouble, order="C")
+    n = A.shape[0]
+    perm = np.zeros(n, dtype=np.int32)
+    if lib.ld_lu(n, A.ctypes.data, perm.ctypes.data):
+        raise np.linalg.LinAlgError("singular matrix (extended LU)")
+    return A, perm
+
+
+def _ext_solve(f, B):
+    lib = _extlib()
+    A, perm = f
+    if lib is None or perm.dtype != np.int32:
+        return _ext_solve_py(f, B)
+    n = A.shape[0]
+    Bm = np.ascontiguousarray(np.asarray(B, np.float64).reshape(n, -1))
+    X = np.empty_like(Bm)
+    lib.ld_lu_solve(n, A.ctypes.data, perm.ctypes.data, Bm.shape[1], Bm.ctypes.data, X.ctypes.data)
+    return X.reshape(np.shape(B))
 
 
 def _lu(K):

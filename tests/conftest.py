@@ -11,3 +11,4 @@ for p in (ROOT, PKG_DIR):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built libgpk.so")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+

@@ -46,6 +46,28 @@ def problem_3d(eq="poisson", kind="Matern52_Cos_1d", ns=(10, 8, 6), Q=4, seed=0,
     return prob, params, fs
 
 
+def config_problem(cid, seed=0, m_test=8):
+    """The oracle problem + params of a BASELINE config (gpk.problems.CONFIGS), the random field
+    seeded exactly as gpk.problems.make_solver seeds it (the bench's inputs); returns
+    (prob, params, (test inputs, test solution), cfg).  m_test=300 is the reference's test grid
+    (code/model_GP_solver_2d.py:369-374, code/model_GP_solver_1d.py:307-312)."""
+    from gpk.problems import CONFIGS
+    cfg = CONFIGS[cid]
+    n = cfg["n"]
+    rng = np.random.default_rng(seed)
+    if cfg["dim"] == 1:
+        prob, Xte, ute = O.setup_1d(cfg["equation"], n, cfg["scale"], cfg["kernel"],
+                                    llk_weight=cfg["llk_weight"], m_test=m_test)
+        params = O.init_params_1d(n, 30, cfg["freq_scale"])
+        params["u"] = 0.1 * rng.normal(size=n).reshape(n, 1)
+    else:
+        prob, Xte, ute = O.setup_2d(cfg["equation"], n, cfg["scale"], cfg["kernel"],
+                                    llk_weight=cfg["llk_weight"], beta=cfg.get("beta"), m_test=m_test)
+        params = O.init_params_2d(n, n, 30, cfg["freq_scale"])
+        params["U"] = 0.1 * rng.normal(size=n * n).reshape(n, n)
+    return prob, params, (Xte, ute), cfg
+
+
 def device_solver(prob, Q, fs=20.0, lr=0.01, flags=0):
     from gpk.core import DeviceSolver
     if "x" in prob:
@@ -69,3 +91,25 @@ def extra_params(rng, n):
     return {"log_tau": 0.1, "log_v": -0.2,
             "kernel_paras": {"log-w": 0.2 * rng.normal(size=1), "log-ls": 0.2 * rng.normal(size=1)},
             "u": 0.05 * rng.normal(size=(n, 1))}
+
+
+def record_parity(test, config, errors, tol=None, extra=None):
+    """Append one line of observed parity errors (per key) to $GPK_PARITY_LOG (default
+    gpurun_out/parity.jsonl): the GPU parity tests' margins, summarised into profiles/r*_parity.json
+    (tools/parity_summary.py).  Never fails a test."""
+    import json
+    import os
+    import time
+    path = os.environ.get("GPK_PARITY_LOG", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity.jsonl"))
+    rec = {"test": test, "config": config, "errors": {k: float(v) for k, v in errors.items()},
+           "time": time.strftime("%Y-%m-%dT%H:%M:%S")}
+    if tol is not None:
+        rec["tol"] = {k: float(v) for k, v in tol.items()} if isinstance(tol, dict) else float(tol)
+    if extra:
+        rec.update(extra)
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    except OSError:
+        pass

@@ -51,3 +51,29 @@ def test_cpu_baseline_child_1d_and_2d(config):
     r = bench.cpu_baseline_child(config, 0.2, 2)
     assert r.get("value") and r["value"] > 0, r
     assert r["cores"] == 2 and r["kind"] == "port" and config in r["sample"]
+
+
+def test_sharded_section_ok_exits_zero():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--dry-run", "--dry-run-sharded", "ok"], env=_env(), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert "dry-run" in out["sharded"]
+
+
+@pytest.mark.parametrize("mode", ["hang", "raise"])
+def test_sharded_section_failure_exits_nonzero(mode):
+    """A stuck collective (the watchdog fires) or a failing rank in the sharded section makes
+    bench.py --gpus 2 exit non-zero, naming the rank and the stage on stderr; rank 0 still prints
+    its line, with the error in `sharded`."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--dry-run", "--dry-run-sharded", mode, "--sharded-timeout", "8"],
+                       env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0, (r.stdout, r.stderr)
+    assert "sharded section FAILED" in r.stderr, r.stderr
+    assert "rank 1" in r.stderr or "rank 0" in r.stderr, r.stderr
+    assert "dry-run sharded" in r.stderr, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert "error" in json.loads(lines[0])["sharded"]

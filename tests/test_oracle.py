@@ -211,6 +211,40 @@ def test_extended_mode_agrees_when_well_conditioned():
     assert rel(O.flatten_params(go), O.flatten_params(gt)) < 1e-12
 
 
+def test_extended_c_kernel_equals_numpy_loops():
+    """oracle/ext_solve.c (blocked, OpenMP) is the same long-double LU as the NumPy loops: same
+    pivots and factors, solves within long-double rounding (blocking reorders the sums)."""
+    if O._extlib() is None:
+        pytest.skip("oracle/_build/libgpk_ext.so not built")
+    rng = np.random.default_rng(3)
+    n = 150                                     # > 2 blocks of 64, ragged last block
+    M = rng.normal(size=(n, n))
+    K = M @ M.T / n + 1e-3 * np.eye(n)
+    B = rng.normal(size=(n, 5))
+    fp, fc = O._ext_lu_py(K), O._ext_lu(K)
+    assert np.array_equal(np.asarray(fp[1]), np.asarray(fc[1]))
+    assert float(np.max(np.abs(fp[0] - fc[0]))) <= 1e-17 * float(np.max(np.abs(fp[0])))
+    xp, xc = O._ext_solve_py(fp, B), O._ext_solve(fc, B)
+    assert rel(xc, xp) < 1e-15
+    assert O._slogdet_from_lu(("ext", fc)) == pytest.approx(O._slogdet_from_lu(("ext", fp)), rel=1e-15)
+
+
+@pytest.mark.parametrize("cid", ["C1", "C3"])
+def test_extended_fixture_reproduces(cid):
+    """tests/golden/ext_<cfg>.npz (tools/solve_accuracy.py --fixture) is what the yardstick
+    gives here: recompute it for the small configs (C1 200-point 1D, C3 128^2)."""
+    import tools.solve_accuracy as SA
+    from tests.helpers import config_problem
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"ext_{cid}.npz"))
+    prob, params, _, _ = config_problem(cid)
+    le, ge = SA.run_mode(prob, params, "ext")
+    ll, gl = SA.run_mode(prob, params, "lu")
+    assert abs(le - float(fx["loss_ext"])) <= 1e-14 * abs(le)
+    for k, v in ge.items():
+        assert rel(v, fx[f"ext/{k}"]) < 1e-13, k
+        assert rel(gl[k], v) == pytest.approx(float(fx[f"lu_err/{k}"]), rel=0.5, abs=1e-15), k
+
+
 def test_adam_matches_optax_formula():
     """optax 0.1.4 scale_by_adam + scale(-lr), eps_root=0, bias correction by count."""
     opt = O.Adam(0.01)

@@ -145,6 +145,35 @@ def test_group_split_factors_matches_unsharded(nranks, big):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nranks,axis", [(2, 2), (4, 1), (3, 2)])
+def test_group_split_factors_non_pd_is_group_wide(nranks, axis):
+    """A factor that is not positive definite is seen on device only by the ranks that invert it;
+    the step sums the status bits over the group, so EVERY rank reports it (group_run checks each
+    rank's status and calls a disagreement an internal error): under RCCL a rank that carried on
+    would enter the next collectives alone and hang.  The handles stay usable afterwards."""
+    from gpk._lib import GPK_FLAG_SPLIT_FACTORS, GPKError, GPK_ENOTPD
+    prob, params, _, fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=72, n2=64, Q=4, seed=8)
+    g = _group(prob, 4, fs, nranks, flags=GPK_FLAG_SPLIT_FACTORS)
+    try:
+        bad = {k: (dict(v) if isinstance(v, dict) else v) for k, v in params.items()}
+        kp = dict(bad[f"kernel_paras_{axis}"])
+        kp["log-w"] = np.array(kp["log-w"], dtype=float)
+        kp["log-w"][0] = np.nan                      # K_axis all NaN: no positive pivot
+        bad[f"kernel_paras_{axis}"] = kp
+        g.set_params(bad)
+        with pytest.raises(GPKError) as ei:
+            g.loss_grad()
+        assert ei.value.code == GPK_ENOTPD, str(ei.value)
+        assert "differs across the ranks" not in str(ei.value)
+        g.set_params(params)                          # recovered: the next call is clean
+        lg, gg = g.loss_grad()
+        lo, go = O.loss_grad_2d(prob, params)
+        assert abs(lg - lo) / abs(lo) < _tol(prob, params)
+    finally:
+        g.close()
+
+
+@pytest.mark.gpu
 def test_group_eight_ranks_c5_split_factors():
     """Eight ranks on the full C5 problem (advection 4096^2, Matern52_Cos, Q = 30) with one
     Kronecker factor per rank half (GPK_FLAG_SPLIT_FACTORS, the 128-wide large-factor inverse):

@@ -48,7 +48,7 @@ for c in a.configs.split(","):
     nfac = 2 if dim == 2 else 1
     dense = 28 * n ** 3 if dim == 2 else n ** 3
     row = {"gpu_it_s": 1 / dt, "ms_per_step": dt * 1e3, "steps": k, "inverse_path": path,
-           "spd_inverse_us": inv_us, "cholesky_gflops": nfac * n ** 3 / (inv_us * 1e-6) / 1e9,
+           "spd_inverse_us": inv_us, "spd_inverse_gflops": nfac * n ** 3 / (inv_us * 1e-6) / 1e9,
            "dense_flops_per_step": dense,
            "mfma_frac_dense": dense / dt / 1e12 / bench.PEAK_F64_TFLOPS}
     print(json.dumps({c: row}), file=sys.stderr, flush=True)
