@@ -88,7 +88,8 @@ __device__ void pivot0(const AssembleArgs& A, unsigned need) {
   __syncthreads();
   const double k00 = P[0];
   if (t == 0 && blockIdx.x == 0) TR_LO(SLOT_PIVOT0);
-  const double ls = pivot_chol_inv_block(P, M, pv, t, A.status);
+  const double ls = pivot_chol_inv_block(P, M, pv, t, A.status);  // (four-wave form: the one-wave
+  // form's accumulators cost gather_kernel, an HBM-bound launch, one wave per SIMD of occupancy)
   if (t == 0 && blockIdx.x == 0) TR_HI(SLOT_PIVOT0);
   for (int e = t; e < 1024; e += 256) A.piv[e] = M[(e >> 5) * SP + (e & 31)];
   if (t == 0) {

@@ -68,6 +68,7 @@ __device__ __forceinline__ double rsqrt_f64(double p) {
 // in between to land (a read at step 4 checked at step 6 stalled every pivot by ~1 us), and a
 // check at step 4 came too early for most inputs (C4: steps 2/5 beat 1/4 by ~1%).
 struct NoPivotHook {
+  __device__ constexpr bool waves() const { return false; }  // (pivot_chol_inv_1w: waves 1-3 skip it)
   __device__ void early() {}
   __device__ void pre() {}
   __device__ void post() {}
@@ -177,6 +178,169 @@ __device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t,
     for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
   }
   __syncthreads();
+  return ls;
+}
+
+
+// The same factorisation by ONE wave (wave 0; waves 1-3 only run the hook), bitwise equal to
+// pivot_chol_inv_block (same operations per element, tools/probes/pivot_variants_probe.hip):
+// wave 0 keeps the lower 16x16 tiles (0,0), (1,0), (1,1) of A and of M in six MFMA accumulators
+// (register r of lane (li, lk) = element (16 I + lk + 4 r, 16 J + li)), so a block step needs no
+// workgroup barrier (LDS operations of one wave are in order), and it publishes to LDS only what
+// the NEXT block step reads -- A's next column block (rows at and below it) and M's next block
+// rows -- instead of every updated entry.  4.3 us against 5.0 us per factorisation.
+// The upper tile of A in LDS is left stale (read only for rows above the block, whose operand is
+// masked to zero); the upper tile of M is zero.  M's LDS copy is complete on return.
+// Hook: wave 0 runs early() after block step 2 and pre() / post() after block step 5, and then
+// raises *sflag (LDS, zero on entry; the caller clears it, see below); waves 1-3 wait for the flag
+// (LDS polling, on their own SIMDs) and then run the three hook calls themselves, so per-thread
+// prefetches (chain_master's PivotPrefetch) are issued at the same point of the factorisation as
+// with the four-wave form.  hook.waves() == false (NoPivotHook): waves 1-3 go straight to the
+// closing barrier.  *sflag is reset to zero by wave 0 after the closing barrier.
+template <typename LP = double*, typename Hook = NoPivotHook>
+__device__ __forceinline__ double pivot_chol_inv_1w(LP A, LP M, LP pv, int t, int* status,
+                                                    volatile int* sflag = nullptr, Hook hook = Hook()) {
+  typedef double dv4 __attribute__((ext_vector_type(4)));
+  double ls = 0.0;
+  if (t < 64) {
+    const int lane = t, li = lane & 15, lk = lane >> 4;
+    dv4 a00, a10, a11, m00, m10, m11;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = lk + 4 * r;
+      a00[r] = A[row * SP + li];
+      a10[r] = A[(16 + row) * SP + li];
+      a11[r] = A[(16 + row) * SP + 16 + li];
+      m00[r] = (row == li) ? 1.0 : 0.0;
+      m10[r] = 0.0;
+      m11[r] = m00[r];
+      M[row * SP + li] = m00[r];
+      M[row * SP + 16 + li] = 0.0;
+      M[(16 + row) * SP + li] = 0.0;
+      M[(16 + row) * SP + 16 + li] = m11[r];
+    }
+    const double s0 = lk == 0 ? 1.0 : 0.0, s1 = lk == 1 ? 1.0 : 0.0, s2 = lk == 2 ? 1.0 : 0.0,
+                 s3 = lk == 3 ? 1.0 : 0.0;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const int b0 = 4 * kb, b1 = b0 + 4, J0 = kb >> 2;
+      double D[4][4], ar0[4], ar1[4], mb0[4], mb1[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y <= x; ++y) D[x][y] = A[(b0 + x) * SP + b0 + y];
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        ar0[z] = J0 == 0 ? A[li * SP + b0 + z] : 0.0;
+        ar1[z] = A[(16 + li) * SP + b0 + z];
+        mb0[z] = M[(b0 + z) * SP + li];
+        mb1[z] = J0 == 1 ? M[(b0 + z) * SP + 16 + li] : 0.0;
+      }
+      // D = L_D L_D^T, W = L_D^{-1}: pivot_chol_inv_block's arithmetic
+      double L[4][4], rinv[4], W[4][4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        double sx = D[x][x];
+#pragma unroll
+        for (int z = 0; z < x; ++z) sx = fma(-L[x][z], L[x][z], sx);
+        if (lane == 0) pv[b0 + x] = sx;
+        rinv[x] = rsqrt_f64(sx);
+#pragma unroll
+        for (int y = x + 1; y < 4; ++y) {
+          double q = D[y][x];
+#pragma unroll
+          for (int z = 0; z < x; ++z) q = fma(-L[y][z], L[x][z], q);
+          L[y][x] = q * rinv[x];
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        W[x][x] = rinv[x];
+#pragma unroll
+        for (int y = x + 1; y < 4; ++y) {
+          double q = 0.0;
+#pragma unroll
+          for (int z = x; z < y; ++z) q = fma(L[y][z], W[z][x], q);
+          W[y][x] = -q * rinv[y];
+        }
+#pragma unroll
+        for (int y = 0; y < x; ++y) W[y][x] = 0.0;
+      }
+      double l0 = 0.0, l1 = 0.0, x0 = 0.0, x1 = 0.0;
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const double w = fma(W[0][z], s0, fma(W[1][z], s1, fma(W[2][z], s2, W[3][z] * s3)));
+        l0 = fma(ar0[z], w, l0);
+        l1 = fma(ar1[z], w, l1);
+        x0 = fma(w, mb0[z], x0);
+        x1 = fma(w, mb1[z], x1);
+      }
+      const double oa0 = (li >= b1) ? -l0 : 0.0, oa1 = (16 + li >= b1) ? -l1 : 0.0;
+      const double ob0 = (li >= b1) ? l0 : 0.0, ob1 = (16 + li >= b1) ? l1 : 0.0;
+      if (J0 == 0) {
+        a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, ob0, a00, 0, 0, 0);
+        a10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob0, a10, 0, 0, 0);
+        m00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, x0, m00, 0, 0, 0);
+      }
+      a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob1, a11, 0, 0, 0);
+      m10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x0, m10, 0, 0, 0);
+      m11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x1, m11, 0, 0, 0);
+      const int rb = kb & 3;  // the block's rows: register rb of tile row J0 (final: M_B = X)
+      if (J0 == 0) {
+        m00[rb] = x0;
+      } else {
+        m10[rb] = x0;
+        m11[rb] = x1;
+      }
+      if (kb < 7) {  // publish what block step kb + 1 reads
+        const int J1 = b1 >> 4, c1 = b1 & 15, r1 = (b1 & 15) >> 2;
+        const bool mine = li >= c1 && li < c1 + 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = lk + 4 * r;
+          if (J1 == 0) {
+            if (mine && row >= b1) A[row * SP + li] = a00[r];
+            if (mine) A[(16 + row) * SP + li] = a10[r];
+          } else {
+            if (mine && 16 + row >= b1) A[(16 + row) * SP + 16 + li] = a11[r];
+          }
+        }
+        if (J1 == 0) {
+          M[(lk + 4 * r1) * SP + li] = m00[r1];
+        } else {
+          M[(16 + lk + 4 * r1) * SP + li] = m10[r1];
+          M[(16 + lk + 4 * r1) * SP + 16 + li] = m11[r1];
+        }
+      }
+      if (kb == 2) hook.early();
+      if (kb == 5) {
+        hook.pre();
+        hook.post();
+        if (hook.waves() && lane == 0) *sflag = 1;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = lk + 4 * r;
+      M[row * SP + li] = m00[r];
+      M[(16 + row) * SP + li] = m10[r];
+      M[(16 + row) * SP + 16 + li] = m11[r];
+    }
+    const double pk = pv[lane & 31];
+    if (lane < 32 && !(pk > 0.0)) atomicOr(status, 1);
+    ls = (lane < 32) ? log(pk) : 0.0;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+  } else if (hook.waves()) {
+    while (*sflag == 0) __builtin_amdgcn_s_sleep(1);  // raised by wave 0 within the call
+    hook.early();
+    hook.pre();
+    hook.post();
+  }
+  __syncthreads();
+  if (hook.waves() && t == 0) *sflag = 0;  // (every wave has seen it: they passed the barrier)
   return ls;
 }
 

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void pivot_init_kernel(SpdBatch b) {
   const int p = b.p[m];
   for (int e = t; e < 1024; e += 256) A[(e >> 5) * SP + (e & 31)] = X[(size_t)(e >> 5) * p + (e & 31)];
   __syncthreads();
-  const double ls = pivot_chol_inv_block(A, M, pv, t, b.status[m]);
+  const double ls = pivot_chol_inv_1w(A, M, pv, t, b.status[m]);
   double* piv = b.piv[m];
   for (int e = t; e < 1024; e += 256) piv[e] = M[(e >> 5) * SP + (e & 31)];
   if (t == 0) {
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(SpdBatch b, int k) {
   }
   __syncthreads();
   if (trb) TR_LO(SLOT_SWEEP_PIVOT + k);
-  const double ls = pivot_chol_inv_block(sP, sM, pv, t, b.status[m]);
+  const double ls = pivot_chol_inv_1w(sP, sM, pv, t, b.status[m]);
   double* piv = b.piv[m] + (size_t)(k + 1) * 1024;
   for (int e = t; e < 1024; e += 256) piv[e] = sM[(e >> 5) * SP + (e & 31)];
   if (t == 0) b.ldet[m][k + 1] = ls;
@@ -278,6 +278,7 @@ __device__ __forceinline__ bool gran_ok(double v) {
 // The pivot chain of one factor (chain_kernel, chain_multi_kernel): one workgroup factors every
 // pivot block in order.  acc: this wave's quadrant of tile (0, 0) of K.  LDS: sXJ [32][SB],
 // sP / sM [32][SP], pv [32].
+template <bool ONEWAVE>
 __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc, double* sXJ,
                                              double* sP, double* sM, double* pv, bool trm,
                                              bool early_flag) {
@@ -285,6 +286,7 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
   const int wr = wv >> 1, wc = wv & 1;
   const int tx = t & 31, ty = t >> 5;
   unsigned int* piv_rdy = F.flags + F.piv_off;
+  __shared__ int s_pflag;  // pivot_chol_inv_1w's "wave 0 passed block step 5" flag
     // (issue priority over the tile workgroup that may share its CU: this one is the chain)
   __builtin_amdgcn_s_setprio(3);
   // The pivot chain, kept in one workgroup: after factoring pivot k it holds L_k^{-1} in LDS,
@@ -307,6 +309,7 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
     }
   };
   struct PivotPrefetch {
+    __device__ constexpr bool waves() const { return true; }  // every thread issues its own words
     decltype(issue)* f;
     int k, T;
     __device__ void early() {}
@@ -325,7 +328,15 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
     if (trm && kp > 0 && kp < 17) TR_LO(SLOT_SWEEP_PIVOT + kp - 1);
     if (trm && kp == 0) TR_LO(SLOT_PIVOT0);
     PivotPrefetch hook{&issue, kp, T};
-    const double ls = pivot_chol_inv_block<4, double*, PivotPrefetch>(sP, sM, pv, t, F.status, hook);
+    // ONEWAVE (chain_kernel): the one-wave factorisation (spd_pivot.h pivot_chol_inv_1w, 4.3 vs
+    // 5.0 us), waves 1-3 issuing their prefetch words when wave 0 passes block step 5;
+    // chain_multi_kernel keeps the four-wave form (its tile path is at the register limit: the
+    // one-wave form's accumulators would spill there)
+    double ls;
+    if (ONEWAVE)
+      ls = pivot_chol_inv_1w<double*, PivotPrefetch>(sP, sM, pv, t, F.status, &s_pflag, hook);
+    else
+      ls = pivot_chol_inv_block<4, double*, PivotPrefetch>(sP, sM, pv, t, F.status, hook);
     for (int e = t; e < 1024; e += 256) st_sc1(F.piv + (size_t)kp * 1024 + e, sM[(e >> 5) * SP + (e & 31)]);
     if (t == 0) F.ldet[kp] = ls;
     if (kp + 1 == T) signal_flag(piv_rdy + kp);
@@ -340,6 +351,7 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(F.pst + 1), 0ull, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (t == 0) s_pflag = 0;  // (the barrier inside factor(0) orders it before the pivot)
   factor(0);  // acc = tile (0, 0) of K, gathered above
   for (int k = 0; k + 1 < T; ++k) {
     // L_k's flag: raised inside the hop (below); with early_flag (chain_multi, whose inputs are
@@ -389,7 +401,7 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
 }
 
 template <int DERIV, bool GATHER>
-__global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
+__global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
   const int m = blockIdx.y;
   if (m == b.nmat) {  // the step constants, off the inverse's critical path
     if (blockIdx.x == 0) publish_prep(b.prep, b.q);
@@ -483,7 +495,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainBatch b) {
   };
   const bool trm = t == 0 && m == 0;  // probes (gpk_trace.h): factor 0's pivot owners
   if (master) {
-    chain_master(F, T, acc, sXJ, sP, sM, pv, trm, false);
+    chain_master<true>(F, T, acc, sXJ, sP, sM, pv, trm, false);
   } else {
     if (trm && tile == 0) TR_LO(SLOT_GATHER);
     chain_inputs(0);                       // tiles (0, 1) and (1, 1) as they are before sweep 0
@@ -747,7 +759,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
     double* sXJ = pool;             // [32][SB]
     double* sP = pool + 32 * SB;    // [32][SP]
     double* sM = sP + 32 * SP;      // [32][SP]
-    chain_master(F, T, a0, sXJ, sP, sM, pv, trm, true);
+    chain_master<false>(F, T, a0, sXJ, sP, sM, pv, trm, true);
   }
 
   // hand-offs after sweep kk - 1 (kk = k + 1; kk = 0: before sweep 0): panel row kk -- tile

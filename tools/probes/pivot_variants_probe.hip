@@ -1,0 +1,589 @@
+// Probe: variants of the 32x32 pivot factorisation (Cholesky + L^{-1}; the pivot chain's serial
+// step, spd_pivot.h pivot_chol_inv_block) -- time per factorisation and bitwise agreement with it.
+//   V0  spd_pivot.h as shipped (4 waves, one barrier per 4-column block step)
+//   V1  V0 + look-ahead: every lane forms the NEXT block step's 4x4 diagonal block itself, during
+//       this step (from the values it already reads + this step's W), so the next 4x4 Cholesky
+//       needs no LDS read and can run under this step's MFMA / LDS write / barrier latency
+//   V2  one wave (64 lanes) holds the lower 16x16 tiles of A and M in MFMA accumulators: no
+//       barriers at all, 6 MFMAs per step
+//   V3  V2 + the look-ahead of V1
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 pivot_variants_probe.hip -o pivot_variants_probe
+#include "../../gaussian-process-slover-for-high-freq-pde_amd/csrc/spd_pivot.h"
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); return 1; } } while (0)
+
+using namespace gpk;
+typedef double dv4 __attribute__((ext_vector_type(4)));
+
+// the 4x4 Cholesky of D (lower part used), rinv, W = L_D^{-1} -- exactly spd_pivot.h's arithmetic
+__device__ __forceinline__ void chol4(const double (&D)[4][4], double (&W)[4][4], double* pv, int b0, bool wr_pv) {
+  double L[4][4], rinv[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    double s = D[x][x];
+#pragma unroll
+    for (int z = 0; z < x; ++z) s = fma(-L[x][z], L[x][z], s);
+    if (wr_pv) pv[b0 + x] = s;
+    rinv[x] = rsqrt_f64(s);
+#pragma unroll
+    for (int y = x + 1; y < 4; ++y) {
+      double q = D[y][x];
+#pragma unroll
+      for (int z = 0; z < x; ++z) q = fma(-L[y][z], L[x][z], q);
+      L[y][x] = q * rinv[x];
+    }
+  }
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    W[x][x] = rinv[x];
+#pragma unroll
+    for (int y = x + 1; y < 4; ++y) {
+      double q = 0.0;
+#pragma unroll
+      for (int z = x; z < y; ++z) q = fma(L[y][z], W[z][x], q);
+      W[y][x] = -q * rinv[y];
+    }
+#pragma unroll
+    for (int y = 0; y < x; ++y) W[y][x] = 0.0;
+  }
+}
+
+// next step's diagonal block: Dn - ln ln^T with ln[x][w] = sum_z An[x][z] W[w][z] (the MFMA's
+// fma order: products k = 0..3 accumulated in sequence onto the old value)
+__device__ __forceinline__ void next_diag(const double (&An)[4][4], const double (&Dn)[4][4],
+                                          const double (&W)[4][4], double (&Dout)[4][4]) {
+  double ln[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      double q = 0.0;
+#pragma unroll
+      for (int z = 0; z < 4; ++z) q = fma(An[x][z], W[w][z], q);
+      ln[x][w] = q;
+    }
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y <= x; ++y) {
+      double q = Dn[x][y];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q = fma(-ln[x][k], ln[y][k], q);
+      Dout[x][y] = q;
+    }
+}
+
+// V1: spd_pivot.h with the diagonal look-ahead
+__device__ __forceinline__ double piv_v1(double* A, double* M, double* pv, int t, int* status) {
+  const int lane = t & 63, wv = t >> 6, wr = wv >> 1, wc = wv & 1;
+  const int li = lane & 15, lk = lane >> 4;
+  const int ri = 16 * wr + li, cj = 16 * wc + li;
+  dv4 accA, accM;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 16 * wr + lk + 4 * r;
+    accA[r] = A[row * SP + cj];
+    accM[r] = (row == cj) ? 1.0 : 0.0;
+    M[row * SP + cj] = accM[r];
+  }
+  const double s0 = lk == 0 ? 1.0 : 0.0, s1 = lk == 1 ? 1.0 : 0.0, s2 = lk == 2 ? 1.0 : 0.0,
+               s3 = lk == 3 ? 1.0 : 0.0;
+  __syncthreads();
+  double D[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y <= x; ++y) D[x][y] = A[x * SP + y];
+#pragma unroll
+  for (int kb = 0; kb < 8; ++kb) {
+    const int b0 = 4 * kb, b1 = b0 + 4;
+    double ar[4], ac[4], mb[4], An[4][4], Dn[4][4];
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+      ar[z] = A[ri * SP + b0 + z];
+      ac[z] = A[cj * SP + b0 + z];
+      mb[z] = M[(b0 + z) * SP + cj];
+    }
+    if (kb < 7) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+#pragma unroll
+        for (int z = 0; z < 4; ++z) An[x][z] = A[(b1 + x) * SP + b0 + z];
+#pragma unroll
+        for (int y = 0; y <= x; ++y) Dn[x][y] = A[(b1 + x) * SP + b1 + y];
+      }
+    }
+    double W[4][4];
+    chol4(D, W, pv, b0, t == 0);
+    double lr = 0.0, lc = 0.0, xv = 0.0;
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+      const double w = fma(W[0][z], s0, fma(W[1][z], s1, fma(W[2][z], s2, W[3][z] * s3)));
+      lr = fma(ar[z], w, lr);
+      lc = fma(ac[z], w, lc);
+      xv = fma(w, mb[z], xv);
+    }
+    const double opa = (ri >= b1) ? -lr : 0.0;
+    const double opb = (cj >= b1) ? lc : 0.0;
+    accA = __builtin_amdgcn_mfma_f64_16x16x4f64(opa, opb, accA, 0, 0, 0);
+    accM = __builtin_amdgcn_mfma_f64_16x16x4f64(opa, xv, accM, 0, 0, 0);
+    if (kb < 7) next_diag(An, Dn, W, D);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * wr + lk + 4 * r;
+      if (16 * wr + 4 * r == b0) accM[r] = xv;
+      if (kb < 7 && row >= b1) {
+        if (cj >= b1) A[row * SP + cj] = accA[r];
+        M[row * SP + cj] = accM[r];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) M[(16 * wr + lk + 4 * r) * SP + cj] = accM[r];
+  double ls = 0.0;
+  if (t < 64) {
+    const double pk = pv[t & 31];
+    if (t < 32 && !(pk > 0.0)) atomicOr(status, 1);
+    ls = (t < 32) ? log(pk) : 0.0;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+  }
+  __syncthreads();
+  return ls;
+}
+
+
+// V4: spd_pivot.h, but each block step publishes only what the NEXT step reads (A's next column
+// block -- rows >= b1 -- and M's next block rows); the other updated entries stay in the
+// accumulators until their column block comes up
+__device__ __forceinline__ double piv_v4(double* A, double* M, double* pv, int t, int* status) {
+  const int lane = t & 63, wv = t >> 6, wr = wv >> 1, wc = wv & 1;
+  const int li = lane & 15, lk = lane >> 4;
+  const int ri = 16 * wr + li, cj = 16 * wc + li;
+  dv4 accA, accM;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 16 * wr + lk + 4 * r;
+    accA[r] = A[row * SP + cj];
+    accM[r] = (row == cj) ? 1.0 : 0.0;
+    M[row * SP + cj] = accM[r];
+  }
+  const double s0 = lk == 0 ? 1.0 : 0.0, s1 = lk == 1 ? 1.0 : 0.0, s2 = lk == 2 ? 1.0 : 0.0,
+               s3 = lk == 3 ? 1.0 : 0.0;
+  __syncthreads();
+#pragma unroll
+  for (int kb = 0; kb < 8; ++kb) {
+    const int b0 = 4 * kb, b1 = b0 + 4;
+    double D[4][4], ar[4], ac[4], mb[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y <= x; ++y) D[x][y] = A[(b0 + x) * SP + b0 + y];
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+      ar[z] = A[ri * SP + b0 + z];
+      ac[z] = A[cj * SP + b0 + z];
+      mb[z] = M[(b0 + z) * SP + cj];
+    }
+    double W[4][4];
+    chol4(D, W, pv, b0, t == 0);
+    double lr = 0.0, lc = 0.0, xv = 0.0;
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+      const double w = fma(W[0][z], s0, fma(W[1][z], s1, fma(W[2][z], s2, W[3][z] * s3)));
+      lr = fma(ar[z], w, lr);
+      lc = fma(ac[z], w, lc);
+      xv = fma(w, mb[z], xv);
+    }
+    const double opa = (ri >= b1) ? -lr : 0.0;
+    const double opb = (cj >= b1) ? lc : 0.0;
+    accA = __builtin_amdgcn_mfma_f64_16x16x4f64(opa, opb, accA, 0, 0, 0);
+    accM = __builtin_amdgcn_mfma_f64_16x16x4f64(opa, xv, accM, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * wr + lk + 4 * r;
+      if (16 * wr + 4 * r == b0) accM[r] = xv;
+      if (kb < 7) {
+        // A's next column block (its rows at and below it; ar / ac of the next step read rows
+        // above it too, but those are masked), M's next block rows
+        if (cj >= b1 && cj < b1 + 4 && row >= b1) A[row * SP + cj] = accA[r];
+        if (16 * wr + 4 * r == b1) M[row * SP + cj] = accM[r];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) M[(16 * wr + lk + 4 * r) * SP + cj] = accM[r];
+  double ls = 0.0;
+  if (t < 64) {
+    const double pk = pv[t & 31];
+    if (t < 32 && !(pk > 0.0)) atomicOr(status, 1);
+    ls = (t < 32) ? log(pk) : 0.0;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+  }
+  __syncthreads();
+  return ls;
+}
+
+// V2 / V3: one wave.  Tiles (I, J) of A and M, I >= J (lower), in accumulators a[I][J], m[I][J]:
+// register r of lane (li, lk) = element (16 I + lk + 4 r, 16 J + li).  The upper tile of A is
+// never maintained (its LDS copy is stale: read only for rows above the block, where the operand
+// is masked to zero); the upper tile of M is zero throughout.
+template <bool LOOKAHEAD, bool NEXTONLY = false>
+__device__ __forceinline__ double piv_1w(double* A, double* M, double* pv, int t, int* status) {
+  double ls = 0.0;
+  if (t < 64) {
+    const int lane = t, li = lane & 15, lk = lane >> 4;
+    dv4 a00, a10, a11, m00, m10, m11;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = lk + 4 * r;
+      a00[r] = A[row * SP + li];
+      a10[r] = A[(16 + row) * SP + li];
+      a11[r] = A[(16 + row) * SP + 16 + li];
+      m00[r] = (row == li) ? 1.0 : 0.0;
+      m10[r] = 0.0;
+      m11[r] = m00[r];
+      M[row * SP + li] = m00[r];
+      M[row * SP + 16 + li] = 0.0;
+      M[(16 + row) * SP + li] = 0.0;
+      M[(16 + row) * SP + 16 + li] = m11[r];
+    }
+    const double s0 = lk == 0 ? 1.0 : 0.0, s1 = lk == 1 ? 1.0 : 0.0, s2 = lk == 2 ? 1.0 : 0.0,
+                 s3 = lk == 3 ? 1.0 : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    double D[4][4];
+    if (LOOKAHEAD) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y <= x; ++y) D[x][y] = A[x * SP + y];
+    }
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const int b0 = 4 * kb, b1 = b0 + 4, J0 = kb >> 2;
+      double ar0[4], ar1[4], mb0[4], mb1[4], An[4][4], Dn[4][4];
+      if (!LOOKAHEAD) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y <= x; ++y) D[x][y] = A[(b0 + x) * SP + b0 + y];
+      }
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        ar0[z] = J0 == 0 ? A[li * SP + b0 + z] : 0.0;
+        ar1[z] = A[(16 + li) * SP + b0 + z];
+        mb0[z] = M[(b0 + z) * SP + li];
+        mb1[z] = J0 == 1 ? M[(b0 + z) * SP + 16 + li] : 0.0;
+      }
+      if (LOOKAHEAD && kb < 7) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+#pragma unroll
+          for (int z = 0; z < 4; ++z) An[x][z] = A[(b1 + x) * SP + b0 + z];
+#pragma unroll
+          for (int y = 0; y <= x; ++y) Dn[x][y] = A[(b1 + x) * SP + b1 + y];
+        }
+      }
+      double W[4][4];
+      chol4(D, W, pv, b0, lane == 0);
+      double l0 = 0.0, l1 = 0.0, x0 = 0.0, x1 = 0.0;
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const double w = fma(W[0][z], s0, fma(W[1][z], s1, fma(W[2][z], s2, W[3][z] * s3)));
+        l0 = fma(ar0[z], w, l0);
+        l1 = fma(ar1[z], w, l1);
+        x0 = fma(w, mb0[z], x0);
+        x1 = fma(w, mb1[z], x1);
+      }
+      const double oa0 = (li >= b1) ? -l0 : 0.0, oa1 = (16 + li >= b1) ? -l1 : 0.0;
+      const double ob0 = (li >= b1) ? l0 : 0.0, ob1 = (16 + li >= b1) ? l1 : 0.0;
+      if (J0 == 0) {
+        a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, ob0, a00, 0, 0, 0);
+        a10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob0, a10, 0, 0, 0);
+        m00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, x0, m00, 0, 0, 0);
+      }
+      a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob1, a11, 0, 0, 0);
+      m10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x0, m10, 0, 0, 0);
+      m11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x1, m11, 0, 0, 0);
+      if (LOOKAHEAD && kb < 7) next_diag(An, Dn, W, D);
+      const int rb = kb & 3;  // register of the block's rows in tile row J0
+      if (J0 == 0) {
+        m00[rb] = x0;
+      } else {
+        m10[rb] = x0;
+        m11[rb] = x1;
+      }
+      if (kb < 7 && NEXTONLY) {
+        // only what the next step reads: A's column block b1 (rows >= b1), M's rows b1..b1+3
+        const int J1 = b1 >> 4, c1 = b1 & 15, r1 = (b1 & 15) >> 2;
+        const bool mine = li >= c1 && li < c1 + 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = lk + 4 * r;
+          if (J1 == 0) {
+            if (mine && row >= b1) A[row * SP + li] = a00[r];
+            if (mine) A[(16 + row) * SP + li] = a10[r];
+          } else {
+            if (mine && 16 + row >= b1) A[(16 + row) * SP + 16 + li] = a11[r];
+          }
+        }
+        if (J1 == 0) {
+          M[(lk + 4 * r1) * SP + li] = m00[r1];
+        } else {
+          M[(16 + lk + 4 * r1) * SP + li] = m10[r1];
+          M[(16 + lk + 4 * r1) * SP + 16 + li] = m11[r1];
+        }
+      } else if (kb < 7) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = lk + 4 * r;
+          if (J0 == 0 && row >= b1) {
+            if (li >= b1) A[row * SP + li] = a00[r];
+            M[row * SP + li] = m00[r];
+          }
+          if (16 + row >= b1) {
+            if (J0 == 0) A[(16 + row) * SP + li] = a10[r];
+            if (16 + li >= b1) A[(16 + row) * SP + 16 + li] = a11[r];
+            M[(16 + row) * SP + li] = m10[r];
+            M[(16 + row) * SP + 16 + li] = m11[r];
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = lk + 4 * r;
+      M[row * SP + li] = m00[r];
+      M[(16 + row) * SP + li] = m10[r];
+      M[(16 + row) * SP + 16 + li] = m11[r];
+    }
+    const double pk = pv[lane & 31];
+    if (lane < 32 && !(pk > 0.0)) atomicOr(status, 1);
+    ls = (lane < 32) ? log(pk) : 0.0;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+  }
+  __syncthreads();
+  return ls;
+}
+
+
+__device__ __forceinline__ double rdlane(double v, int src) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), src);
+  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), src);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// V6..: one wave, next-block writes only, with options
+//   SEL  pick W's row lk by selects instead of 0/1-weighted fmas
+//   RDL  the 4x4 diagonal block straight from the accumulators (v_readlane) instead of LDS
+template <bool SEL, bool RDL>
+__device__ __forceinline__ double piv_1w2(double* A, double* M, double* pv, int t, int* status) {
+  double ls = 0.0;
+  if (t < 64) {
+    const int lane = t, li = lane & 15, lk = lane >> 4;
+    dv4 a00, a10, a11, m00, m10, m11;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = lk + 4 * r;
+      a00[r] = A[row * SP + li];
+      a10[r] = A[(16 + row) * SP + li];
+      a11[r] = A[(16 + row) * SP + 16 + li];
+      m00[r] = (row == li) ? 1.0 : 0.0;
+      m10[r] = 0.0;
+      m11[r] = m00[r];
+      M[row * SP + li] = m00[r];
+      M[row * SP + 16 + li] = 0.0;
+      M[(16 + row) * SP + li] = 0.0;
+      M[(16 + row) * SP + 16 + li] = m11[r];
+    }
+    const double s0 = lk == 0 ? 1.0 : 0.0, s1 = lk == 1 ? 1.0 : 0.0, s2 = lk == 2 ? 1.0 : 0.0,
+                 s3 = lk == 3 ? 1.0 : 0.0;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const int b0 = 4 * kb, b1 = b0 + 4, J0 = kb >> 2, c0 = b0 & 15;
+      double D[4][4], ar0[4], ar1[4], mb0[4], mb1[4];
+      if (RDL) {
+        const dv4& aj = J0 == 0 ? a00 : a11;
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y <= x; ++y) D[x][y] = rdlane(aj[kb & 3], 16 * x + c0 + y);
+      } else {
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y <= x; ++y) D[x][y] = A[(b0 + x) * SP + b0 + y];
+      }
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        ar0[z] = J0 == 0 ? A[li * SP + b0 + z] : 0.0;
+        ar1[z] = A[(16 + li) * SP + b0 + z];
+        mb0[z] = M[(b0 + z) * SP + li];
+        mb1[z] = J0 == 1 ? M[(b0 + z) * SP + 16 + li] : 0.0;
+      }
+      double W[4][4];
+      chol4(D, W, pv, b0, lane == 0);
+      double l0 = 0.0, l1 = 0.0, x0 = 0.0, x1 = 0.0;
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const double w = SEL ? (lk == 0 ? W[0][z] : lk == 1 ? W[1][z] : lk == 2 ? W[2][z] : W[3][z])
+                             : fma(W[0][z], s0, fma(W[1][z], s1, fma(W[2][z], s2, W[3][z] * s3)));
+        l0 = fma(ar0[z], w, l0);
+        l1 = fma(ar1[z], w, l1);
+        x0 = fma(w, mb0[z], x0);
+        x1 = fma(w, mb1[z], x1);
+      }
+      const double oa0 = (li >= b1) ? -l0 : 0.0, oa1 = (16 + li >= b1) ? -l1 : 0.0;
+      const double ob0 = (li >= b1) ? l0 : 0.0, ob1 = (16 + li >= b1) ? l1 : 0.0;
+      if (J0 == 0) {
+        a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, ob0, a00, 0, 0, 0);
+        a10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob0, a10, 0, 0, 0);
+        m00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, x0, m00, 0, 0, 0);
+      }
+      a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob1, a11, 0, 0, 0);
+      m10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x0, m10, 0, 0, 0);
+      m11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x1, m11, 0, 0, 0);
+      const int rb = kb & 3;
+      if (J0 == 0) {
+        m00[rb] = x0;
+      } else {
+        m10[rb] = x0;
+        m11[rb] = x1;
+      }
+      if (kb < 7) {
+        const int J1 = b1 >> 4, c1 = b1 & 15, r1 = (b1 & 15) >> 2;
+        const bool mine = li >= c1 && li < c1 + 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = lk + 4 * r;
+          if (J1 == 0) {
+            if (mine && row >= b1) A[row * SP + li] = a00[r];
+            if (mine) A[(16 + row) * SP + li] = a10[r];
+          } else {
+            if (mine && 16 + row >= b1) A[(16 + row) * SP + 16 + li] = a11[r];
+          }
+        }
+        if (J1 == 0) {
+          M[(lk + 4 * r1) * SP + li] = m00[r1];
+        } else {
+          M[(16 + lk + 4 * r1) * SP + li] = m10[r1];
+          M[(16 + lk + 4 * r1) * SP + 16 + li] = m11[r1];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = lk + 4 * r;
+      M[row * SP + li] = m00[r];
+      M[(16 + row) * SP + li] = m10[r];
+      M[(16 + row) * SP + 16 + li] = m11[r];
+    }
+    const double pk = pv[lane & 31];
+    if (lane < 32 && !(pk > 0.0)) atomicOr(status, 1);
+    ls = (lane < 32) ? log(pk) : 0.0;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+  }
+  __syncthreads();
+  return ls;
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void bench(const double* Kin, double* out, int reps, long long* cyc, int* st) {
+  __shared__ double A[32 * SP], M[32 * SP], pv[32];
+  const int t = threadIdx.x;
+  double ls = 0.0;
+  long long tot = 0;
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int e = t; e < 1024; e += 256) A[(e >> 5) * SP + (e & 31)] = Kin[e];
+    __syncthreads();
+    const long long t0 = wall_clock64();
+    double l;
+    if (V == 0) l = pivot_chol_inv_block(A, M, pv, t, st);
+    else if (V == 1) l = piv_v1(A, M, pv, t, st);
+    else if (V == 2) l = piv_1w<false>(A, M, pv, t, st);
+    else if (V == 3) l = piv_1w<true>(A, M, pv, t, st);
+    else if (V == 4) l = piv_v4(A, M, pv, t, st);
+    else if (V == 5) l = piv_1w<false, true>(A, M, pv, t, st);
+    else if (V == 6) l = piv_1w2<true, false>(A, M, pv, t, st);
+    else if (V == 7) l = piv_1w2<false, true>(A, M, pv, t, st);
+    else l = piv_1w2<true, true>(A, M, pv, t, st);
+    tot += wall_clock64() - t0;
+    ls += l;
+  }
+  for (int e = t; e < 1024; e += 256) out[e] = M[(e >> 5) * SP + (e & 31)];
+  if (t == 0) { out[1024] = ls / reps; cyc[0] = tot; }
+}
+
+template <int V>
+int run(const char* name, const double* dK, double* dout, long long* cyc, int* st, int rate,
+        std::vector<double>& res) {
+  const int reps = 400;
+  hipLaunchKernelGGL(bench<V>, dim3(1), dim3(256), 0, 0, dK, dout, reps, cyc, st);
+  CHK(hipDeviceSynchronize());
+  hipLaunchKernelGGL(bench<V>, dim3(1), dim3(256), 0, 0, dK, dout, reps, cyc, st);
+  CHK(hipDeviceSynchronize());
+  long long c;
+  CHK(hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost));
+  res.assign(1025, 0.0);
+  CHK(hipMemcpy(res.data(), dout, 1025 * 8, hipMemcpyDeviceToHost));
+  printf("  V%d %-40s %.3f us per factorisation\n", V, name, (double)c / reps / (rate * 1e-3));
+  return 0;
+}
+
+int main() {
+  int rate = 0;
+  CHK(hipDeviceGetAttribute(&rate, hipDeviceAttributeWallClockRate, 0));
+  double *dK, *dout;
+  long long* cyc;
+  int* st;
+  CHK(hipMalloc(&dK, 8192)); CHK(hipMalloc(&dout, 1025 * 8)); CHK(hipMalloc(&cyc, 16)); CHK(hipMalloc(&st, 16));
+  for (int pass = 0; pass < 2; ++pass) {
+    const double jit = pass == 0 ? 1e-3 : 1e-6, h = pass == 0 ? 0.07 : 0.0245;
+    std::vector<double> K(1024);
+    for (int i = 0; i < 32; ++i)
+      for (int j = 0; j < 32; ++j) {
+        double d = fabs((double)(i - j)) * h;
+        K[i * 32 + j] = (1 + sqrt(5.0) * d + 5.0 / 3.0 * d * d) * exp(-sqrt(5.0) * d) * cos(3.0 * d) + (i == j ? jit : 0.0);
+      }
+    CHK(hipMemcpy(dK, K.data(), 8192, hipMemcpyHostToDevice));
+    CHK(hipMemset(st, 0, 16));
+    printf("pivot variants, 32x32, jitter %.0e (wall clock %d kHz)\n", jit, rate);
+    std::vector<double> r0, r;
+    run<0>("spd_pivot.h (4 waves, barriers)", dK, dout, cyc, st, rate, r0);
+    auto cmp = [&](int v) {
+      int nd = 0;
+      double mx = 0.0;
+      for (int e = 0; e < 1025; ++e) {
+        if (memcmp(&r[e], &r0[e], 8)) ++nd;
+        mx = fmax(mx, fabs(r[e] - r0[e]) / fmax(fabs(r0[e]), 1e-300));
+      }
+      printf("     V%d vs V0: %d of 1025 values differ (max rel %.2e); logdet %.17g vs %.17g\n", v, nd, mx, r[1024], r0[1024]);
+    };
+    run<1>("+ look-ahead diagonal", dK, dout, cyc, st, rate, r); cmp(1);
+    run<2>("one wave, no barriers", dK, dout, cyc, st, rate, r); cmp(2);
+    run<3>("one wave + look-ahead", dK, dout, cyc, st, rate, r); cmp(3);
+    run<4>("4 waves, next-block writes only", dK, dout, cyc, st, rate, r); cmp(4);
+    run<5>("one wave, next-block writes only", dK, dout, cyc, st, rate, r); cmp(5);
+    run<6>("V5 + select W row", dK, dout, cyc, st, rate, r); cmp(6);
+    run<7>("V5 + diagonal by readlane", dK, dout, cyc, st, rate, r); cmp(7);
+    run<8>("V5 + both", dK, dout, cyc, st, rate, r); cmp(8);
+    run<0>("spd_pivot.h (again)", dK, dout, cyc, st, rate, r);
+    int s = 0;
+    CHK(hipMemcpy(&s, st, 4, hipMemcpyDeviceToHost));
+    printf("  status %d\n", s);
+  }
+  return 0;
+}
