@@ -255,20 +255,107 @@ __global__ __launch_bounds__(256) void gather_kernel(AssembleBatch b) {
   if (TR_LAST) TR_HI(SLOT_GATHER_START);
 }
 
+// Launch 2, large factors (no pivot-0 workgroup: the large-factor inverse factors its own
+// pivots): the same element values as gather_kernel, laid out for HBM streaming -- a workgroup
+// covers 8 rows x 512 columns, each lane two adjacent columns (8-B class-id pairs in, 16-B K / Kc /
+// D pairs out, whole 1-KiB row segments per wave instruction), all 8 of a lane's class-id loads
+// issued before its gathers and stores (memory-level parallelism), nontemporal stores.  C5 (two
+// 4096^2 factors): 940 MB per launch (K, Kc, D written, the ids read).
+constexpr int GW_ROWS = 8, GW_COLS = 512;
+constexpr int GW_WIDE_MIN_TILES = 1024;  // 32x32 tiles: P >= 1024
+template <int DERIV>
+__global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b) {
+  const int axis = blockIdx.z;
+  const AssembleArgs& A = b.ax[axis];
+  const ClassArgs& C = A.cls;
+  const int p = A.p;
+  const int r0 = blockIdx.y * GW_ROWS, c0 = blockIdx.x * GW_COLS;
+  if (r0 >= p || c0 >= p) return;  // (the shorter axis)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int2 id[2][4];
+  int row[2], col[4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    row[h] = r0 + w + 4 * h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      col[q] = c0 + 128 * q + 2 * lane;
+      id[h][q] = (col[q] < p) ? *reinterpret_cast<const int2*>(C.cid + (size_t)row[h] * p + col[q])
+                              : make_int2(-1, -1);
+    }
+  }
+  double xi[2] = {0.0, 0.0};
+  double2 xj[4];
+  if (DERIV == 1) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) xi[h] = A.x[min(row[h], A.n - 1)];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      xj[q] = make_double2(A.x[min(col[q], A.n - 1)], A.x[min(col[q] + 1, A.n - 1)]);
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (col[q] >= p) continue;
+      const int i = row[h];
+      double kv[2], dv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int u = e == 0 ? id[h][q].x : id[h][q].y, j = col[q] + e;
+        if (u >= 0) {
+          kv[e] = C.kval[u];
+          if (i == j) kv[e] += A.jitter;
+          dv[e] = C.dval[u];
+          if (DERIV == 1) {
+            const double xjj = e == 0 ? xj[q].x : xj[q].y;
+            if (!(xi[h] - xjj >= 0.0)) dv[e] = -dv[e];  // JAX abs'(0) = +1
+          }
+        } else {
+          kv[e] = (i == j) ? 1.0 : 0.0;
+          dv[e] = 0.0;
+        }
+      }
+      // nontemporal stores: 3.4 -> 7.0 TB/s at C5 size (tools/probes/gather_probe.hip; write-
+      // allocating stores held the launch at 3.4-3.7 TB/s whatever the layout); the next readers
+      // (the inverse, the GEMMs) run on other XCDs and read from memory anyway
+      // (one 16-B store per array and lane: per-element stores interleaved across the arrays
+      // were not merged and ran at 1.9 TB/s)
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      const size_t o = (size_t)i * p + col[q];
+      const d2v k2 = {kv[0], kv[1]}, d2 = {dv[0], dv[1]};
+      __builtin_nontemporal_store(k2, reinterpret_cast<d2v*>(A.K + o));
+      if (A.Kc) __builtin_nontemporal_store(k2, reinterpret_cast<d2v*>(A.Kc + o));
+      if (DERIV) __builtin_nontemporal_store(d2, reinterpret_cast<d2v*>(A.D + o));
+    }
+}
+
+static void launch_gather_wide(const AssembleBatch& b, int naxes, int deriv, hipStream_t s) {
+  int pmax = 0;
+  for (int k = 0; k < naxes; ++k) pmax = std::max(pmax, b.ax[k].p);
+  dim3 g((pmax + GW_COLS - 1) / GW_COLS, (pmax + GW_ROWS - 1) / GW_ROWS, naxes);
+  if (deriv == 2) hipLaunchKernelGGL((gather_wide_kernel<2>), g, dim3(256), 0, s, b);
+  else if (deriv == 1) hipLaunchKernelGGL((gather_wide_kernel<1>), g, dim3(256), 0, s, b);
+  else hipLaunchKernelGGL((gather_wide_kernel<0>), g, dim3(256), 0, s, b);
+}
+
 template <bool MATERN, bool COS>
 static void launch_class_t(const AssembleBatch& b, int naxes, int maxc, int maxtiles, int q,
                            int deriv, hipStream_t s, bool eval_only) {
   dim3 ge((maxc + 7) / 8, naxes), gg(naxes, maxtiles + (b.pivot_x >= 0 ? 1 : 0));
+  // (no pivot-0 workgroup and large tiles: the streaming layout)
+  const bool wide = b.pivot_x < 0 && maxtiles >= GW_WIDE_MIN_TILES;
   if (deriv == 2) {
     hipLaunchKernelGGL((class_eval_kernel<MATERN, COS, 2>), ge, dim3(256), 0, s, b, q);
-    if (!eval_only) hipLaunchKernelGGL((gather_kernel<2>), gg, dim3(256), 0, s, b);
+    if (!eval_only && !wide) hipLaunchKernelGGL((gather_kernel<2>), gg, dim3(256), 0, s, b);
   } else if (deriv == 1) {
     hipLaunchKernelGGL((class_eval_kernel<MATERN, COS, 1>), ge, dim3(256), 0, s, b, q);
-    if (!eval_only) hipLaunchKernelGGL((gather_kernel<1>), gg, dim3(256), 0, s, b);
+    if (!eval_only && !wide) hipLaunchKernelGGL((gather_kernel<1>), gg, dim3(256), 0, s, b);
   } else {
     hipLaunchKernelGGL((class_eval_kernel<MATERN, COS, 0>), ge, dim3(256), 0, s, b, q);
-    if (!eval_only) hipLaunchKernelGGL((gather_kernel<0>), gg, dim3(256), 0, s, b);
+    if (!eval_only && !wide) hipLaunchKernelGGL((gather_kernel<0>), gg, dim3(256), 0, s, b);
   }
+  if (!eval_only && wide) launch_gather_wide(b, naxes, deriv, s);
 }
 
 // the gather launch alone (gpk_bench_kernel "gather": the K-assembly kernel's HBM rate); the
@@ -282,6 +369,10 @@ hipError_t launch_gather_only(const AssembleArgs* a, int naxes, hipStream_t s) {
     maxtiles = std::max(maxtiles, (a[k].p / 32) * (a[k].p / 32));
   }
   b.pivot_x = -1;
+  if (maxtiles >= GW_WIDE_MIN_TILES) {  // (what launch_assemble runs at this size)
+    launch_gather_wide(b, naxes, a[0].deriv, s);
+    return hipGetLastError();
+  }
   dim3 gg(naxes, maxtiles);
   if (a[0].deriv == 2) hipLaunchKernelGGL((gather_kernel<2>), gg, dim3(256), 0, s, b);
   else if (a[0].deriv == 1) hipLaunchKernelGGL((gather_kernel<1>), gg, dim3(256), 0, s, b);
