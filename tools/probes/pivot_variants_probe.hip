@@ -386,7 +386,7 @@ __device__ __forceinline__ double rdlane(double v, int src) {
 // V6..: one wave, next-block writes only, with options
 //   SEL  pick W's row lk by selects instead of 0/1-weighted fmas
 //   RDL  the 4x4 diagonal block straight from the accumulators (v_readlane) instead of LDS
-template <bool SEL, bool RDL>
+template <bool SEL, bool RDL, bool NOCHOL = false, int MF = 0>
 __device__ __forceinline__ double piv_1w2(double* A, double* M, double* pv, int t, int* status) {
   double ls = 0.0;
   if (t < 64) {
@@ -433,7 +433,14 @@ __device__ __forceinline__ double piv_1w2(double* A, double* M, double* pv, int 
         mb1[z] = J0 == 1 ? M[(b0 + z) * SP + 16 + li] : 0.0;
       }
       double W[4][4];
-      chol4(D, W, pv, b0, lane == 0);
+      if (NOCHOL) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y) W[x][y] = (x == y) ? 1.0 + D[x][x] * 1e-30 : 1e-3;
+      } else {
+        chol4(D, W, pv, b0, lane == 0);
+      }
       double l0 = 0.0, l1 = 0.0, x0 = 0.0, x1 = 0.0;
 #pragma unroll
       for (int z = 0; z < 4; ++z) {
@@ -446,15 +453,32 @@ __device__ __forceinline__ double piv_1w2(double* A, double* M, double* pv, int 
       }
       const double oa0 = (li >= b1) ? -l0 : 0.0, oa1 = (16 + li >= b1) ? -l1 : 0.0;
       const double ob0 = (li >= b1) ? l0 : 0.0, ob1 = (16 + li >= b1) ? l1 : 0.0;
-      if (J0 == 0) {
-        a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, ob0, a00, 0, 0, 0);
-        a10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob0, a10, 0, 0, 0);
-        m00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, x0, m00, 0, 0, 0);
+      if (MF == 1) {  // no MFMAs (timing only)
+        a00[0] += oa0 * ob0; a10[0] += oa1; m00[0] += x0; a11[0] += ob1; m10[0] += x1;
+      } else if (MF == 2) {  // the tiles the next step reads first, the others after its writes
+        if (J0 == 0) {
+          a10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob0, a10, 0, 0, 0);
+          a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, ob0, a00, 0, 0, 0);
+          m00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, x0, m00, 0, 0, 0);
+        } else {
+          a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob1, a11, 0, 0, 0);
+          m10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x0, m10, 0, 0, 0);
+          m11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x1, m11, 0, 0, 0);
+        }
+      } else {
+        if (J0 == 0) {
+          a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, ob0, a00, 0, 0, 0);
+          a10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob0, a10, 0, 0, 0);
+          m00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, x0, m00, 0, 0, 0);
+        }
+        a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob1, a11, 0, 0, 0);
+        m10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x0, m10, 0, 0, 0);
+        m11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x1, m11, 0, 0, 0);
       }
-      a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob1, a11, 0, 0, 0);
-      m10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x0, m10, 0, 0, 0);
-      m11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x1, m11, 0, 0, 0);
       const int rb = kb & 3;
+      if (MF == 2 && J0 == 0) {  // (M rows of tile row 1 are read from step 4 on)
+        m10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x0, m10, 0, 0, 0);
+      }
       if (J0 == 0) {
         m00[rb] = x0;
       } else {
@@ -481,6 +505,9 @@ __device__ __forceinline__ double piv_1w2(double* A, double* M, double* pv, int 
           M[(16 + lk + 4 * r1) * SP + 16 + li] = m11[r1];
         }
       }
+      if (MF == 2 && J0 == 0) {  // tile (1, 1): read from step 4 on (a11's column blocks)
+        a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob1, a11, 0, 0, 0);
+      }
       __builtin_amdgcn_wave_barrier();
     }
 #pragma unroll
@@ -500,10 +527,175 @@ __device__ __forceinline__ double piv_1w2(double* A, double* M, double* pv, int 
   return ls;
 }
 
+
+// V9: pipelined two-wave form.  Wave 1 runs the serial chain of 4x4 factorisations one block step
+// AHEAD: W_k needs only W_{k-1} and two 4x4 blocks as they were after MFMA step k-2 (D_k =
+// A_kk - l l^T with l = A_{k,k-1} W_{k-1}^T, the MFMA's fma order), which wave 0 hands over in
+// per-step LDS slots (no reuse: no write-after-read race).  Wave 0 does the MFMA updates (V5) with
+// W_k from LDS.  The waves meet through two LDS counters (W's ready, MFMA steps done), no barrier.
+__device__ __forceinline__ double piv_pipe(double* A, double* M, double* pv, double* Wb, double* Hb,
+                                           volatile int* fl, int t, int* status) {
+  double ls = 0.0;
+  const int lane = t & 63, wv = t >> 6;
+  if (wv == 1) {  // ---- the 4x4 chain (all lanes redundant; same values) ----
+    double D[4][4], An[4][4], Dn[4][4], Wp[4][4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y <= x; ++y) D[x][y] = A[x * SP + y];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {  // step 1's inputs: still the initial values
+#pragma unroll
+      for (int z = 0; z < 4; ++z) An[x][z] = A[(4 + x) * SP + z];
+#pragma unroll
+      for (int y = 0; y <= x; ++y) Dn[x][y] = A[(4 + x) * SP + 4 + y];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int b = 4 * k;
+      if (k >= 1) {
+        if (k >= 2) {
+          while (fl[1] < k - 1) {}
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+#pragma unroll
+            for (int z = 0; z < 4; ++z) An[x][z] = Hb[k * 32 + 4 * x + z];
+#pragma unroll
+            for (int y = 0; y <= x; ++y) Dn[x][y] = Hb[k * 32 + 16 + 4 * x + y];
+          }
+        }
+        next_diag(An, Dn, Wp, D);
+      }
+      double W[4][4];
+      chol4(D, W, pv, b, lane == 0);
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          Wb[k * 16 + 4 * x + z] = W[x][z];
+          Wp[x][z] = W[x][z];
+        }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      fl[0] = k + 1;
+    }
+  } else if (wv == 0) {  // ---- the MFMA updates ----
+    const int li = lane & 15, lk = lane >> 4;
+    dv4 a00, a10, a11, m00, m10, m11;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = lk + 4 * r;
+      a00[r] = A[row * SP + li];
+      a10[r] = A[(16 + row) * SP + li];
+      a11[r] = A[(16 + row) * SP + 16 + li];
+      m00[r] = (row == li) ? 1.0 : 0.0;
+      m10[r] = 0.0;
+      m11[r] = m00[r];
+      M[row * SP + li] = m00[r];
+      M[row * SP + 16 + li] = 0.0;
+      M[(16 + row) * SP + li] = 0.0;
+      M[(16 + row) * SP + 16 + li] = m11[r];
+    }
+    const double s0 = lk == 0 ? 1.0 : 0.0, s1 = lk == 1 ? 1.0 : 0.0, s2 = lk == 2 ? 1.0 : 0.0,
+                 s3 = lk == 3 ? 1.0 : 0.0;
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const int b0 = 4 * kb, b1 = b0 + 4, J0 = kb >> 2;
+      double ar0[4], ar1[4], mb0[4], mb1[4];
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        ar0[z] = J0 == 0 ? A[li * SP + b0 + z] : 0.0;
+        ar1[z] = A[(16 + li) * SP + b0 + z];
+        mb0[z] = M[(b0 + z) * SP + li];
+        mb1[z] = J0 == 1 ? M[(b0 + z) * SP + 16 + li] : 0.0;
+      }
+      while (fl[0] < kb + 1) {}
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      double wr[4];
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        wr[z] = fma(Wb[kb * 16 + z], s0, fma(Wb[kb * 16 + 4 + z], s1, fma(Wb[kb * 16 + 8 + z], s2, Wb[kb * 16 + 12 + z] * s3)));
+      double l0 = 0.0, l1 = 0.0, x0 = 0.0, x1 = 0.0;
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        l0 = fma(ar0[z], wr[z], l0);
+        l1 = fma(ar1[z], wr[z], l1);
+        x0 = fma(wr[z], mb0[z], x0);
+        x1 = fma(wr[z], mb1[z], x1);
+      }
+      const double oa0 = (li >= b1) ? -l0 : 0.0, oa1 = (16 + li >= b1) ? -l1 : 0.0;
+      const double ob0 = (li >= b1) ? l0 : 0.0, ob1 = (16 + li >= b1) ? l1 : 0.0;
+      if (J0 == 0) {
+        a00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, ob0, a00, 0, 0, 0);
+        a10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob0, a10, 0, 0, 0);
+        m00 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa0, x0, m00, 0, 0, 0);
+      }
+      a11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, ob1, a11, 0, 0, 0);
+      m10 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x0, m10, 0, 0, 0);
+      m11 = __builtin_amdgcn_mfma_f64_16x16x4f64(oa1, x1, m11, 0, 0, 0);
+      const int rb = kb & 3;
+      if (J0 == 0) {
+        m00[rb] = x0;
+      } else {
+        m10[rb] = x0;
+        m11[rb] = x1;
+      }
+      // hand-over to wave 1 for W_{kb+2}: A_{kb+2,kb+1} and A_{kb+2,kb+2} as of this step
+      if (kb + 2 <= 7) {
+        const int k2 = kb + 2, bk = 4 * k2, bp = bk - 4;
+        const int I = bk >> 4, Jp = bp >> 4, r2 = (bk & 15) >> 2, cp = bp & 15, ck = bk & 15;
+        const dv4& tA = (I == 0) ? a00 : (Jp == 0 ? a10 : a11);   // tile (I, Jp)
+        const dv4& tD = (I == 0) ? a00 : a11;                    // tile (I, I)
+        if (li >= cp && li < cp + 4) Hb[k2 * 32 + 4 * lk + li - cp] = tA[r2];
+        if (li >= ck && li < ck + 4) Hb[k2 * 32 + 16 + 4 * lk + li - ck] = tD[r2];
+      }
+      if (kb < 7) {
+        const int J1 = b1 >> 4, c1 = b1 & 15, r1 = (b1 & 15) >> 2;
+        const bool mine = li >= c1 && li < c1 + 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = lk + 4 * r;
+          if (J1 == 0) {
+            if (mine && row >= b1) A[row * SP + li] = a00[r];
+            if (mine) A[(16 + row) * SP + li] = a10[r];
+          } else {
+            if (mine && 16 + row >= b1) A[(16 + row) * SP + 16 + li] = a11[r];
+          }
+        }
+        if (J1 == 0) {
+          M[(lk + 4 * r1) * SP + li] = m00[r1];
+        } else {
+          M[(16 + lk + 4 * r1) * SP + li] = m10[r1];
+          M[(16 + lk + 4 * r1) * SP + 16 + li] = m11[r1];
+        }
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      fl[1] = kb + 1;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = lk + 4 * r;
+      M[row * SP + li] = m00[r];
+      M[(16 + row) * SP + li] = m10[r];
+      M[(16 + row) * SP + 16 + li] = m11[r];
+    }
+    const double pk = pv[lane & 31];
+    if (lane < 32 && !(pk > 0.0)) atomicOr(status, 1);
+    ls = (lane < 32) ? log(pk) : 0.0;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+  }
+  __syncthreads();
+  if (t == 0) { fl[0] = 0; fl[1] = 0; }
+  return ls;
+}
+
 template <int V>
 __global__ __launch_bounds__(256) void bench(const double* Kin, double* out, int reps, long long* cyc, int* st) {
-  __shared__ double A[32 * SP], M[32 * SP], pv[32];
+  __shared__ double A[32 * SP], M[32 * SP], pv[32], Wb[8 * 16], Hb[8 * 32];
+  __shared__ int fl[2];
   const int t = threadIdx.x;
+  if (t == 0) { fl[0] = 0; fl[1] = 0; }
   double ls = 0.0;
   long long tot = 0;
   for (int rep = 0; rep < reps; ++rep) {
@@ -519,7 +711,11 @@ __global__ __launch_bounds__(256) void bench(const double* Kin, double* out, int
     else if (V == 5) l = piv_1w<false, true>(A, M, pv, t, st);
     else if (V == 6) l = piv_1w2<true, false>(A, M, pv, t, st);
     else if (V == 7) l = piv_1w2<false, true>(A, M, pv, t, st);
-    else l = piv_1w2<true, true>(A, M, pv, t, st);
+    else if (V == 8) l = piv_1w2<true, true>(A, M, pv, t, st);
+    else if (V == 9) l = piv_pipe(A, M, pv, Wb, Hb, fl, t, st);
+    else if (V == 10) l = piv_1w2<false, false, true>(A, M, pv, t, st);
+    else if (V == 11) l = piv_1w2<false, false, false, 1>(A, M, pv, t, st);
+    else l = piv_1w2<false, false, false, 2>(A, M, pv, t, st);
     tot += wall_clock64() - t0;
     ls += l;
   }
@@ -579,7 +775,10 @@ int main() {
     run<5>("one wave, next-block writes only", dK, dout, cyc, st, rate, r); cmp(5);
     run<6>("V5 + select W row", dK, dout, cyc, st, rate, r); cmp(6);
     run<7>("V5 + diagonal by readlane", dK, dout, cyc, st, rate, r); cmp(7);
-    run<8>("V5 + both", dK, dout, cyc, st, rate, r); cmp(8);
+    run<9>("pipelined: wave 1 4x4 chain, wave 0 MFMA", dK, dout, cyc, st, rate, r); cmp(9);
+    run<10>("V5 without the 4x4 factorisation (timing)", dK, dout, cyc, st, rate, r);
+    run<11>("V5 without MFMAs (timing)", dK, dout, cyc, st, rate, r);
+    run<12>("V5, next step's tiles' MFMAs first", dK, dout, cyc, st, rate, r); cmp(12);
     run<0>("spd_pivot.h (again)", dK, dout, cyc, st, rate, r);
     int s = 0;
     CHK(hipMemcpy(&s, st, 4, hipMemcpyDeviceToHost));
