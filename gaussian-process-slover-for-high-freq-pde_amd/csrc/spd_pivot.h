@@ -191,12 +191,12 @@ __device__ __forceinline__ double pivot_chol_inv_block(LP A, LP M, LP pv, int t,
 // rows -- instead of every updated entry.  4.3 us against 5.0 us per factorisation.
 // The upper tile of A in LDS is left stale (read only for rows above the block, whose operand is
 // masked to zero); the upper tile of M is zero.  M's LDS copy is complete on return.
-// Hook: wave 0 runs early() after block step 2 and pre() / post() after block step 5, and then
-// raises *sflag (LDS, zero on entry; the caller clears it, see below); waves 1-3 wait for the flag
-// (LDS polling, on their own SIMDs) and then run the three hook calls themselves, so per-thread
+// Hook: wave 0 runs early() after block step 2 and pre() / post() after block step 5, then meets
+// waves 1-3 at ONE workgroup barrier (they wait there instead of polling LDS, which competed
+// with wave 0's LDS traffic) and they run the three hook calls themselves, so per-thread
 // prefetches (chain_master's PivotPrefetch) are issued at the same point of the factorisation as
 // with the four-wave form.  hook.waves() == false (NoPivotHook): waves 1-3 go straight to the
-// closing barrier.  *sflag is reset to zero by wave 0 after the closing barrier.
+// closing barrier.  (sflag: unused, kept for the call signature.)
 template <typename LP = double*, typename Hook = NoPivotHook>
 __device__ __forceinline__ double pivot_chol_inv_1w(LP A, LP M, LP pv, int t, int* status,
                                                     volatile int* sflag = nullptr, Hook hook = Hook()) {
@@ -317,7 +317,7 @@ __device__ __forceinline__ double pivot_chol_inv_1w(LP A, LP M, LP pv, int t, in
       if (kb == 5) {
         hook.pre();
         hook.post();
-        if (hook.waves() && lane == 0) *sflag = 1;
+        if (hook.waves()) __syncthreads();  // releases waves 1-3 (waiting there, not polling)
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -334,13 +334,12 @@ __device__ __forceinline__ double pivot_chol_inv_1w(LP A, LP M, LP pv, int t, in
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
   } else if (hook.waves()) {
-    while (*sflag == 0) __builtin_amdgcn_s_sleep(1);  // raised by wave 0 within the call
+    __syncthreads();  // wave 0 has passed block step 5
     hook.early();
     hook.pre();
     hook.post();
   }
   __syncthreads();
-  if (hook.waves() && t == 0) *sflag = 0;  // (every wave has seen it: they passed the barrier)
   return ls;
 }
 
