@@ -99,6 +99,10 @@ struct gpk_handle {
   AxisConst* kc = nullptr;
   StepScalars* sc = nullptr;
   int *count = nullptr, *loss_slot = nullptr, *status = nullptr;
+  // batch begin / report folded into the next enqueued step (capture_call, capture_calln): the
+  // step that takes one clears its pointer
+  const StepBegin* fold_begin = nullptr;
+  const StepReport* fold_report = nullptr;
   double *losses = nullptr, *diag = nullptr;
   double* stat_x = nullptr;  // [2] status bits as doubles (split-factor group all-reduce)
 
@@ -324,6 +328,13 @@ static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
   const bool eval_only = h->chain && h->cls[0].ncls > 0;
   PrepArgs prep = make_prep(h, apply), prep_eval = prep;
   prep_eval.skip = eval_only ? 1 : 0;
+  if (eval_only && h->fold_begin) {  // the batch begin rides on the chain launch's prep row
+    const StepBegin& b = *h->fold_begin;
+    prep.snap = b.snap; prep.snap_m = b.m; prep.snap_v = b.v; prep.snap_np = b.np;
+    prep.snap_count = b.snap ? b.snap_count : nullptr;
+    prep.viol0 = b.viol; prep.slot0 = b.loss_slot;
+    h->fold_begin = nullptr;
+  }
   TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, prep_eval, h->s, eval_only),
                    "assemble"));
   mark(h, 1);
@@ -371,6 +382,11 @@ static TailArgs make_tail(gpk_handle* h, int apply, bool refine = true) {
   if (!refine) {  // fast graph: check that no refinement was needed
     for (int a = 0; a < L.naxes; ++a) f.watch[a] = h->pst[a];
     f.viol = h->viol;
+  }
+  if (h->fold_report) {
+    f.report = 1;
+    f.rep = *h->fold_report;
+    h->fold_report = nullptr;
   }
   AdamUArgs& au = T.adam;
   au.L = L; au.hyper = h->hyper; au.llk_weight = h->prob.llk_weight; au.apply = apply; au.ac = ac;
@@ -1029,6 +1045,28 @@ static StepReport make_report(gpk_handle* h, bool fast, int nloss) {
   return r;
 }
 
+// Batch begin for the graph being captured: folded into the first step's chain launch when
+// that launch publishes the step constants (publish_prep, copy_snapshot), else its own launch.
+static int begin_batch(gpk_handle* h, const StepBegin* b) {
+  if (!h->shard && h->chain && h->cls[0].ncls > 0) {
+    h->fold_begin = b;
+    return GPK_OK;
+  }
+  return check_launch(launch_step_begin(*b, h->s), "step_begin");
+}
+
+// Batch end: the last step's loss workgroup wrote the report (make_tail took fold_report), or
+// the report kernel runs after it.  Leaves no fold pending (also when the capture failed: rc).
+static int end_batch(gpk_handle* h, const StepReport* r, int rc) {
+  const bool pending_begin = h->fold_begin != nullptr, pending_report = h->fold_report != nullptr;
+  h->fold_begin = nullptr;
+  h->fold_report = nullptr;
+  if (rc != GPK_OK) return rc;
+  if (pending_begin) return fail(GPK_EINVAL, "internal: the batch begin was not folded into a step");
+  if (pending_report || h->shard) return check_launch(launch_step_report(*r, h->s), "step_report");
+  return GPK_OK;
+}
+
 // one step(1) call: begin (snapshot when fast) + step + report, captured once per graph kind
 static int capture_call(gpk_handle* h, bool fast) {
   hipGraphExec_t* slot = &h->g_call[fast ? 0 : 1];
@@ -1042,9 +1080,13 @@ static int capture_call(gpk_handle* h, bool fast) {
     b.snap_count = h->snap_count; b.count = h->count; b.viol = h->viol;
   }
   b.loss_slot = h->loss_slot;
-  int rc = check_launch(launch_step_begin(b, h->s), "step_begin");
-  if (rc == GPK_OK) rc = enqueue_step(h, 1, !fast);
-  if (rc == GPK_OK) rc = check_launch(launch_step_report(make_report(h, fast, 1), h->s), "step_report");
+  const StepReport r = make_report(h, fast, 1);
+  int rc = begin_batch(h, &b);
+  if (rc == GPK_OK) {
+    if (!h->shard) h->fold_report = &r;
+    rc = enqueue_step(h, 1, !fast);
+  }
+  rc = end_batch(h, &r, rc);
   hipError_t e = hipStreamEndCapture(h->s, &g);
   if (rc != GPK_OK) {
     if (g) (void)hipGraphDestroy(g);
@@ -1068,9 +1110,13 @@ static int capture_calln(gpk_handle* h, int reps) {
   b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
   b.snap_count = h->snap_count; b.count = h->count; b.viol = h->viol;
   b.loss_slot = h->loss_slot;
-  int rc = check_launch(launch_step_begin(b, h->s), "step_begin");
-  for (int r = 0; r < reps && rc == GPK_OK; ++r) rc = enqueue_step(h, 1, false);
-  if (rc == GPK_OK) rc = check_launch(launch_step_report(make_report(h, true, reps), h->s), "step_report");
+  const StepReport rep = make_report(h, true, reps);
+  int rc = begin_batch(h, &b);
+  for (int r = 0; r < reps && rc == GPK_OK; ++r) {
+    if (r == reps - 1 && !h->shard) h->fold_report = &rep;
+    rc = enqueue_step(h, 1, false);
+  }
+  rc = end_batch(h, &rep, rc);
   hipError_t e = hipStreamEndCapture(h->s, &g);
   if (rc != GPK_OK) {
     if (g) (void)hipGraphDestroy(g);

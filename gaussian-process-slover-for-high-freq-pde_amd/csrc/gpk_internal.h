@@ -100,6 +100,11 @@ struct PrepArgs {
   int nb, dim, n1, n2, p2;
   double* bgap;        // out [1]
   int skip;            // 1: this launch does not publish them (another launch of the step does)
+  // first step of a batch, folded in (stepk.h StepBegin; all null otherwise): snap_count <- count
+  // before this step's increment, *viol0 = 0, *slot0 = 0 (thread 0 of publish_prep), and the
+  // rollback snapshot of (params, m, v) copied by the publishing launch's spare workgroups
+  int* snap_count; unsigned int* viol0; int* slot0;
+  double* snap; const double* snap_m; const double* snap_v; size_t snap_np;
 };
 
 // Distance classes.  Every field of a stationary kernel depends on the pair (i, j) only

@@ -16,6 +16,17 @@ __device__ __forceinline__ void axis_component(const PrepArgs& P, int axis, int 
   w = exp(P.params[off + 2 * q + c]);       // log-w
 }
 
+// the rollback snapshot of a folded batch begin (PrepArgs.snap), spread over nwg workgroups
+__device__ inline void copy_snapshot(const PrepArgs& P, int wg, int nwg) {
+  if (!P.snap) return;
+  const size_t np = P.snap_np;
+  for (size_t i = (size_t)wg * blockDim.x + threadIdx.x; i < np; i += (size_t)nwg * blockDim.x) {
+    P.snap[i] = P.params[i];
+    P.snap[np + i] = P.snap_m[i];
+    P.snap[2 * np + i] = P.snap_v[i];
+  }
+}
+
 // workgroup (0, 0): publish the step constants for the later kernels of the step
 __device__ inline void publish_prep(const PrepArgs& P, int q) {
   if (P.skip) return;  // published by another launch of the step
@@ -31,7 +42,10 @@ __device__ inline void publish_prep(const PrepArgs& P, int q) {
   if (t == 0) {
     P.sc->tau = exp(P.params[P.off_tau]);
     P.sc->v = exp(P.params[P.off_v]);
-    const int n = *P.count + 1;
+    const int c0 = *P.count, n = c0 + 1;
+    if (P.snap_count) *P.snap_count = c0;
+    if (P.viol0) *P.viol0 = 0u;
+    if (P.slot0) *P.slot0 = 0;
     if (P.apply) *P.count = n;
     P.sc->bc1 = 1.0 - pow(P.b1, (double)n);
     P.sc->bc2 = 1.0 - pow(P.b2, (double)n);

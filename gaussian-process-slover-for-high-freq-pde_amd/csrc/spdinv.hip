@@ -403,8 +403,9 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
 template <int DERIV, bool GATHER>
 __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
   const int m = blockIdx.y;
-  if (m == b.nmat) {  // the step constants, off the inverse's critical path
+  if (m == b.nmat) {  // the step constants (+ a folded batch begin), off the critical path
     if (blockIdx.x == 0) publish_prep(b.prep, b.q);
+    copy_snapshot(b.prep, blockIdx.x, gridDim.x);
     return;
   }
   const ChainFactor& F = b.f[m];
@@ -671,8 +672,9 @@ __host__ __device__ inline int multi_workgroups(int T) {  // per factor, + the p
 template <int DERIV, bool GATHER>
 __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
   const int m = blockIdx.y;
-  if (m == b.nmat) {
+  if (m == b.nmat) {  // the step constants (+ a folded batch begin), off the critical path
     if (blockIdx.x == 0) publish_prep(b.prep, b.q);
+    copy_snapshot(b.prep, blockIdx.x, gridDim.x);
     return;
   }
   const ChainFactor& F = b.f[m];

@@ -19,6 +19,22 @@ struct AdamHyper {
   double lr, b1, b2, eps;
 };
 
+// Per-batch bookkeeping around the steps of one host call (gpk_step): begin = the rollback
+// snapshot and counter resets before the first step, report = the end-of-batch record.  Graphs
+// fold both into step launches where they can (PrepArgs.snap*, FinalizeArgs.report); the
+// kernels below run them on their own otherwise.
+struct StepBegin {
+  double* snap; const double* params; const double* m; const double* v; size_t np;
+  int* snap_count; const int* count;
+  unsigned int* viol;   // nullable
+  int* loss_slot;
+};
+struct StepReport {
+  const int* status; const unsigned int* viol;  // viol nullable
+  const double* pst[2];                         // nullable per axis
+  const double* losses; int nloss;              // the batch's losses -> out[8 ..]
+  double* out;                                  // [8 + nloss], pinned host memory
+};
 struct FinalizeArgs {
   Layout L;
   AdamHyper hyper;
@@ -41,6 +57,9 @@ struct FinalizeArgs {
   // and an open one raises *viol, after which the host rolls the batch back and reruns it
   // with the refinement stages (gpk_step).  watch[a] = nullptr: not checked.
   const double* watch[2]; unsigned int* viol;
+  // last step of a batch in a captured call: the loss workgroup writes the batch report itself
+  // (after this step's loss), in place of a separate step_report launch
+  int report; StepReport rep;
 };
 
 struct AdamUArgs {
@@ -74,18 +93,6 @@ struct TailArgs {
   int tg, ngpa;              // blocks per group, groups per axis
 };
 
-struct StepBegin {
-  double* snap; const double* params; const double* m; const double* v; size_t np;
-  int* snap_count; const int* count;
-  unsigned int* viol;   // nullable
-  int* loss_slot;
-};
-struct StepReport {
-  const int* status; const unsigned int* viol;  // viol nullable
-  const double* pst[2];                         // nullable per axis
-  const double* losses; int nloss;              // the batch's losses -> out[8 ..]
-  double* out;                                  // [8 + nloss], pinned host memory
-};
 hipError_t launch_step_begin(const StepBegin& b, hipStream_t s);
 hipError_t launch_step_report(const StepReport& r, hipStream_t s);
 

@@ -134,6 +134,21 @@ __device__ inline void finalize_body(const FinalizeArgs& f, int part = 0) {
     *f.loss_slot = slot + 1;
     double* diag = f.diag;
     diag[0] = loss; diag[1] = ld[0]; diag[2] = ld[1]; diag[3] = quad; diag[4] = egap; diag[5] = bgap;
+    if (f.report) {  // this step's loss and the batch header (stepk.hip step_report_kernel's record)
+      const StepReport& r = f.rep;
+      r.out[8 + slot] = loss;
+      r.out[0] = (double)__hip_atomic_load(const_cast<int*>(r.status), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r.out[1] = r.viol ? (double)__hip_atomic_load(const_cast<unsigned int*>(r.viol), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 0.0;
+      for (int a = 0; a < 2; ++a) {
+        r.out[2 + 2 * a] = r.pst[a] ? r.pst[a][0] : 0.0;
+        r.out[3 + 2 * a] = r.pst[a] ? r.pst[a][1] : 0.0;
+      }
+    }
+  }
+  if (do_loss && f.report) {  // the batch's earlier losses (written by earlier launches)
+    for (int k = t; k < f.rep.nloss - 1; k += blockDim.x) f.rep.out[8 + k] = f.rep.losses[k];
+    __threadfence_system();
   }
   __syncthreads();
   if (t == 0) FIN_PROBE(57);
