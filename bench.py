@@ -136,8 +136,10 @@ def large_factors(steps=3):
     try:
         s.prepare(steps)
         s.step(1)
+        s.sync()
         t0 = time.perf_counter()
         s.step(steps)
+        s.sync()
         step_ms = (time.perf_counter() - t0) / steps * 1e3
         us, fl, _ = s.bench_kernel("gemm_B", 5)
         inv_us = s.time_spd_inverse(3)
@@ -178,10 +180,12 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
             STAGE["name"] = f"sharded {key}: prepare + warm-up"
             s.prepare(steps)
             s.step(2)
+            s.sync()
             replicas.barrier(ctx)
             STAGE["name"] = f"sharded {key}: {steps} timed steps"
             t0 = time.perf_counter()
             s.step(steps)
+            s.sync()
             t1 = time.perf_counter()
             replicas.barrier(ctx)
         finally:
@@ -266,6 +270,9 @@ class _DryRunSolver:
         time.sleep(1e-4 * n)
         return [float(self.seed)] * n
 
+    def sync(self):
+        pass
+
     def graph_mode(self):
         return False, 0
 
@@ -334,10 +341,12 @@ def main():
     s = _DryRunSolver(rank) if a.dry_run else make_solver(a.config, seed=rank, device=local)
     s.prepare(a.steps)                   # every graph the timed call can launch, built untimed
     s.step(a.warmup)                     # warm-up steps
+    s.sync()
     replicas.barrier(ctx)
     t0 = time.perf_counter()
     fast_graph, rb0 = s.graph_mode()     # graph the timed batch starts on (refinement gate closed?)
-    losses = s.step(a.steps)             # exactly K steps; returns after a device sync
+    losses = s.step(a.steps)             # exactly K steps (returns once their losses are final)
+    s.sync()                             # ... and the device has finished the last update
     t1 = time.perf_counter()
     replicas.barrier(ctx)
     fast_end, rb1 = s.graph_mode()       # graph it ends on; chunks rerun inside the timed batch
@@ -349,9 +358,11 @@ def main():
     if not a.dry_run:
         # the reference's loop shape: one step() call per iteration (model_GP_solver_2d.py:285-300)
         s.step(5)
+        s.sync()
         t = time.perf_counter()
         for _ in range(a.step1_calls):
             s.step(1)
+        s.sync()
         extra["step1_per_call"] = {"value": a.step1_calls / (time.perf_counter() - t), "unit": "iters/s",
                                    "calls": a.step1_calls}
         # fp64 SPD inverse rate.  The path forms K^{-1} itself (Gauss-Jordan sweeps with Cholesky

@@ -1865,6 +1865,39 @@ static int run_steps(gpk_handle* h, int n_steps, double* losses, bool fast, bool
 constexpr int FAST_CHUNK = 64;
 constexpr int kBatchMax = FAST_CHUNK;  // largest prepared batch graph
 
+// A whole-call graph (capture_call / capture_calln) ends its report with the ready word
+// rep_host[7] (stepk_dev.h report_ready): the host waits for that word instead of the stream, so
+// gpk_step returns as soon as the call's losses and status are final -- the last step's dL/dU and
+// Adam on U may still run, ordered before anything later enqueued on the handle's stream.  The
+// wait polls the stream every few thousand reads, so a faulted or finished-without-report stream
+// ends it.
+static void arm_report(gpk_handle* h) {
+  reinterpret_cast<volatile double*>(h->rep_host)[7] = 0.0;
+}
+
+static int wait_report(gpk_handle* h) {
+  volatile double* ready = reinterpret_cast<volatile double*>(h->rep_host) + 7;
+  for (unsigned it = 1;; ++it) {
+    if (*ready != 0.0) break;
+    if ((it & 4095u) == 0) {
+      const hipError_t e = hipStreamQuery(h->s);
+      if (e == hipErrorNotReady) continue;
+      if (e != hipSuccess) return fail(GPK_EHIP, std::string("step graph: ") + hipGetErrorString(e));
+      if (*ready != 0.0) break;
+      return fail(GPK_EHIP, "internal: the step graph finished without its report");
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return GPK_OK;
+}
+
+int gpk_sync(gpk_handle* h) {
+  if (!h) return fail(GPK_EINVAL, "NULL handle");
+  DevSwitch ds(h->dev);
+  HIPCHK(hipStreamSynchronize(h->s));
+  return GPK_OK;
+}
+
 int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
   if (!h) return fail(GPK_EINVAL, "NULL handle");
   if (n_steps < 0) return fail(GPK_EINVAL, "n_steps < 0");
@@ -1875,8 +1908,9 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
   if (n_steps == 1 && !h->shard) {  // one graph launch per call (a rollback takes the path below)
     const bool fast = h->fast_ok && h->fast_mode;
     TRY(capture_call(h, fast));
+    arm_report(h);
     HIPCHK(hipGraphLaunch(h->g_call[fast ? 0 : 1], h->s));
-    HIPCHK(hipStreamSynchronize(h->s));
+    TRY(wait_report(h));
     if (losses) std::memcpy(losses, h->rep_host + 8, sizeof(double));
     bool viol = false;
     TRY(read_report(h, fast, &viol));
@@ -1888,8 +1922,9 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
     HIPCHK(hipMemcpyAsync(h->count, h->snap_count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
     TRY(check_launch(launch_sync_u(h->params, h->L, h->Up, h->s), "sync_u"));
     TRY(capture_call(h, false));
+    arm_report(h);
     HIPCHK(hipGraphLaunch(h->g_call[1], h->s));
-    HIPCHK(hipStreamSynchronize(h->s));
+    TRY(wait_report(h));
     if (losses) std::memcpy(losses, h->rep_host + 8, sizeof(double));
     return read_report(h, false, &viol);
   }
@@ -1900,8 +1935,9 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
     bool viol = false;
     auto cg = fast && !h->shard ? h->g_calln.find(n) : h->g_calln.end();
     if (cg != h->g_calln.end() && cg->second) {  // a prepared whole-chunk graph
+      arm_report(h);
       HIPCHK(hipGraphLaunch(cg->second, h->s));
-      HIPCHK(hipStreamSynchronize(h->s));
+      TRY(wait_report(h));
       h->pend_losses = lo;
       h->pend_n = n;
       TRY(read_report(h, true, &viol));

@@ -179,6 +179,7 @@ __global__ void step_report_kernel(StepReport r) {
   for (int k = threadIdx.x; k < r.nloss; k += blockDim.x) r.out[8 + k] = r.losses[k];
   if (threadIdx.x != 0) {
     __threadfence_system();
+    __syncthreads();
     return;
   }
   r.out[0] = (double)*r.status;
@@ -188,6 +189,8 @@ __global__ void step_report_kernel(StepReport r) {
     r.out[3 + 2 * a] = r.pst[a] ? r.pst[a][1] : 0.0;  // (bits of max diag K^{-1})
   }
   __threadfence_system();
+  __syncthreads();
+  report_ready(r.out);
 }
 
 hipError_t launch_step_report(const StepReport& r, hipStream_t s) {

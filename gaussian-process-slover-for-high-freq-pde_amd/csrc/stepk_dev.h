@@ -40,6 +40,14 @@ __device__ inline double block_sum(double v, double* sh) {
 // kernel-parameter gradient: the fused tail runs it in a workgroup of its own at the start of
 // the launch); 2 = the kernel-parameter gradients from f.pg and their Adam (the tail's last
 // workgroup, right after it has reduced pg).
+// The report's ready word (out[7]), stored last at system scope: the host returns from gpk_step
+// once it reads 1 (the rest of the launch -- dL/dU and Adam on U -- is stream-ordered before any
+// later call on the handle)
+__device__ __forceinline__ void report_ready(double* out) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(out + 7), 0x3ff0000000000000ull,
+                     __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ inline void finalize_body(const FinalizeArgs& f, int part = 0) {
   const bool do_loss = part != 2, do_kp = part != 1;
   __shared__ double sh[4], sld[2], sg[2];
@@ -151,6 +159,7 @@ __device__ inline void finalize_body(const FinalizeArgs& f, int part = 0) {
     __threadfence_system();
   }
   __syncthreads();
+  if (t == 0 && do_loss && f.report) report_ready(f.rep.out);  // after every thread's fence
   if (t == 0) FIN_PROBE(57);
   // ---- phase 2: gradients (kernel params: the fields were contracted without the weight w_q)
   // and Adam on the small parameters

@@ -92,6 +92,7 @@ EXPORTS = {
     "gpk_loss_grad": ([ctypes.c_void_p, _dp, _dp], ctypes.c_int),
     "gpk_step": ([ctypes.c_void_p, ctypes.c_int32, _dp], ctypes.c_int),
     "gpk_prepare": ([ctypes.c_void_p, ctypes.c_int32], ctypes.c_int),
+    "gpk_sync": ([ctypes.c_void_p], ctypes.c_int),
     "gpk_predict": ([ctypes.c_void_p, _dp, ctypes.c_int32, _dp, ctypes.c_int32, _dp], ctypes.c_int),
     "gpk_criterion": ([ctypes.c_void_p, _dp], ctypes.c_int),
     "gpk_profile_stages": ([ctypes.c_void_p, ctypes.c_int32, _dp, ctypes.c_int32, _ip], ctypes.c_int),

@@ -203,6 +203,10 @@ class DeviceSolver:
         """Build every step graph a step(n) call can launch, without stepping (gpk_prepare)."""
         check(_lib.load().gpk_prepare(self._h, int(n)))
 
+    def sync(self):
+        """Wait for the handle's device work (gpk_sync); step() returns once its losses are known."""
+        check(_lib.load().gpk_sync(self._h))
+
     def predict(self, xte1, xte2=None):
         x1 = f64(xte1).reshape(-1)
         if self.dim == 1:
@@ -313,6 +317,11 @@ class DeviceGroup(DeviceSolver):
     def __init__(self, nranks, *args, **kw):
         self.nranks = int(nranks)
         super().__init__(*args, **kw)
+
+    def sync(self):
+        lib = _lib.load()
+        for k in range(self.nranks):
+            check(lib.gpk_sync(ctypes.c_void_p(self._hs[k])))
 
     def _create(self, lib, p, freq_scale, shard):
         arr = (ctypes.c_void_p * self.nranks)()

@@ -200,8 +200,14 @@ int gpk_loss_grad(gpk_handle* h, double* loss, double* grad_flat);
 
 /* n_steps x step() (model_GP_solver_2d.py:176-183): loss + full gradient + Adam update,
  * params and Adam state device-resident.  losses[n_steps] receives the loss evaluated
- * BEFORE each update (as step() returns it); may be NULL. */
+ * BEFORE each update (as step() returns it); may be NULL.  Returns once the losses and the
+ * device status of the call are final: the last step's U update may still be running, like
+ * the reference's asynchronously dispatched jax step; every later call on the handle is ordered
+ * after it, and gpk_sync waits for it. */
 int gpk_step(gpk_handle* h, int32_t n_steps, double* losses);
+
+/* Wait until every launch enqueued on the handle has finished (timing). */
+int gpk_sync(gpk_handle* h);
 
 /* Capture and instantiate every step graph a gpk_step(n_steps) call can launch (full and fast,
  * single-step and multi-step) without running a step: graph construction is a one-time host

@@ -155,3 +155,29 @@ def test_single_step_call_graph_rollback(name):
         assert np.array_equal(a, b)
     full.close()
     fast.close()
+
+
+def test_step_returns_on_report_and_later_calls_are_ordered():
+    """Whole-call graphs fold the batch begin into the chain launch and the report into the last
+    step's loss workgroup, and gpk_step returns on the report's ready word -- before the last
+    step's U update has finished.  Everything after it on the handle is stream-ordered: state read
+    right after step(1) is the state after the update, and 20 x step(1) is bitwise step(20)."""
+    from gpk.problems import make_solver
+    a = make_solver("C4", seed=0)
+    b = make_solver("C4", seed=0)
+    try:
+        a.prepare(20)
+        la = np.concatenate([a.step(1) for _ in range(20)])
+        early = _state(a)  # no sync: ordered after the last call's tail on the handle's stream
+        a.sync()
+        for x, y in zip(early, _state(a)):
+            assert np.array_equal(x, y)
+        b.prepare(20)
+        lb = b.step(20)
+        assert np.array_equal(la, lb)
+        for x, y in zip(_state(a), _state(b)):
+            assert np.array_equal(x, y)
+        assert np.all(np.isfinite(la))
+    finally:
+        a.close()
+        b.close()

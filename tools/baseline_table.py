@@ -38,8 +38,10 @@ for c in a.configs.split(","):
         k = STEPS[c]
         s.prepare(k)
         s.step(max(5, k // 10))
+        s.sync()
         t0 = time.perf_counter()
         s.step(k)
+        s.sync()
         dt = (time.perf_counter() - t0) / k
         inv_us = s.time_spd_inverse(5 if c == "C5" else 20)
         path = s.inverse_path()

@@ -16,20 +16,26 @@ s = problems.make_solver("C4", seed=0)
 s.prepare(20)
 s.step(5)
 for i in range(4):
+    s.sync()
     t = time.perf_counter()
     s.step(20)
+    s.sync()
     dt = time.perf_counter() - t
     print(f"bench shape call {i}: {dt * 1e6:9.1f} us = {20 / dt:7.1f} it/s", flush=True)
 for i in range(3):  # a 20-step call right after a 5-step one (the exec launched before)
     s.step(5)
+    s.sync()
     t = time.perf_counter()
     s.step(20)
+    s.sync()
     dt = time.perf_counter() - t
     print(f"after step(5) {i}: {dt * 1e6:9.1f} us = {20 / dt:7.1f} it/s", flush=True)
 for i in range(3):  # ... after an idle host pause
     time.sleep(0.05)
+    s.sync()
     t = time.perf_counter()
     s.step(20)
+    s.sync()
     dt = time.perf_counter() - t
     print(f"after 50 ms idle {i}: {dt * 1e6:9.1f} us = {20 / dt:7.1f} it/s", flush=True)
 for n in sizes:
@@ -38,8 +44,10 @@ s.step(80)
 for n in sizes:
     ts = []
     for _ in range(12):
+        s.sync()
         t = time.perf_counter()
         s.step(n)
+        s.sync()
         ts.append(time.perf_counter() - t)
     ts = np.array(ts[2:]) * 1e6
     print(f"step({n:3d}): median {np.median(ts):9.1f} us  min {ts.min():9.1f} us  "

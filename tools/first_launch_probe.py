@@ -8,7 +8,7 @@ for n in (20, 24, 28):
     s.prepare(n)
 s.step(5)
 def call(n):
-    t = time.perf_counter(); s.step(n); return (time.perf_counter() - t) * 1e6
+    s.sync(); t = time.perf_counter(); s.step(n); s.sync(); return (time.perf_counter() - t) * 1e6
 w = [call(20) for _ in range(6)]
 print("warm 20-step calls:", [round(x) for x in w])
 print("first 24-step call right after (no idle):", round(call(24)), " second:", round(call(24)), " per-step est:", round((w[-1]-25)/20, 2))

@@ -13,6 +13,6 @@ ap.add_argument("--flags", type=int, default=0, help="GPK_FLAG_* bits (include/g
 a = ap.parse_args()
 s = problems.make_solver(a.config, seed=0, flags=a.flags)
 s.step(5)
-t = time.perf_counter(); s.step(a.steps); dt = time.perf_counter() - t
+s.sync(); t = time.perf_counter(); s.step(a.steps); s.sync(); dt = time.perf_counter() - t
 print(f"{a.config} flags={a.flags}: {a.steps} steps {dt*1e3/a.steps:.3f} ms/step  {a.steps/dt:.1f} it/s")
 print(s.profile_stages(10))
