@@ -752,7 +752,45 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvDesc d) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int row = blockIdx.x * 4 + wv;
   double acc = 0.0;
-  if (row < d.rows) {
+  if (row < d.rows && d.cid) {
+    // class operand: the same element pairs and summation order as the matrix form below (lane
+    // c takes columns 2c, 2c+1), the pair's two ids in one 8-B load, their values gathered from
+    // the class table (L2-resident); ids first, then values, then the FMAs
+    const int2* ids = reinterpret_cast<const int2*>(d.cid + (size_t)row * d.lda);
+    const double2* xv = reinterpret_cast<const double2*>(d.x);
+    const int n2 = d.p >> 1;
+    auto val = [&](int u, int col) {
+      double v = u >= 0 ? d.cv[u] : 0.0;
+      if (col == row) v = u >= 0 ? (d.ident ? v + d.cdiag : v) : (d.ident ? 1.0 : 0.0);
+      return v;
+    };
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    int c = lane;
+    for (; c + 192 < n2; c += 256) {
+      int2 iv[4];
+      double2 bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        iv[u] = ids[c + 64 * u];
+        bv[u] = xv[c + 64 * u];
+      }
+      double2 av[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int col = 2 * (c + 64 * u);
+        av[u] = make_double2(val(iv[u].x, col), val(iv[u].y, col + 1));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] = fma(av[u].y, bv[u].y, fma(av[u].x, bv[u].x, s[u]));
+    }
+    for (; c < n2; c += 64) {
+      const int2 iv = ids[c];
+      const double2 bv = xv[c];
+      const double ax = val(iv.x, 2 * c), ay = val(iv.y, 2 * c + 1);
+      s[0] = fma(ay, bv.y, fma(ax, bv.x, s[0]));
+    }
+    acc = (s[0] + s[1]) + (s[2] + s[3]);
+  } else if (row < d.rows) {
     // 16-B loads (p and lda are multiples of 32), 8 per lane in flight before the FMAs, four
     // independent partial sums (a serial chain held one load round trip per 64 columns)
     const double2* a = reinterpret_cast<const double2*>(d.A + (size_t)row * d.lda);

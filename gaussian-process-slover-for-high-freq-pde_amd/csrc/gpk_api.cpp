@@ -131,6 +131,9 @@ struct gpk_handle {
   bool bigspd = false;                // large-factor SPD inverse (spdinv_big.hip)
   bool bigwide = false;               // ... with 128-wide sweeps
   bool chain_multi = false;           // persistent inverse on macro tiles (large 1D factors)
+  // large 1D factors with distance classes: the GEMVs read Kc and D as class ids + class values
+  // (GemvDesc::cid), so the inverse launch's gather writes neither matrix (64 MB at C2)
+  bool cls_gemv = false;
   double* Zp[2] = {};                 // ... its double-buffered panel [2][128][P]
   bool chain = false;                 // small factors: persistent one-launch inverse (chain_kernel)
   bool chain_aug = false;             // ... which also solves A, Bt^T and K^{-1} D^T (2D, unsharded)
@@ -274,6 +277,7 @@ static hipError_t launch_chain(gpk_handle* h, bool gather, double** fin, bool au
       c.x = a == 0 ? h->x1 : h->x2; c.jitter = h->prob.jitter; c.Kc = h->Kc[a];
     }
     c.D = h->D[a];  // gather: written; read mode: the augmented D^T columns read it
+    if (gather && h->cls_gemv) c.Kc = c.D = nullptr;  // (the GEMVs read them as classes)
     if (h->chain_aug && aug) {  // axis 0: [U | D1^T] -> A, K1^{-1} D1^T;  axis 1: [U^T | D2^T] -> Bt^T, P2
       const int Po = a == 0 ? L.p2 : L.p1;
       c.tu = Po / 32; c.td = c.p / 32;
@@ -399,6 +403,17 @@ static TailArgs make_tail(gpk_handle* h, int apply, bool refine = true) {
   return T;
 }
 
+// A GEMV operand that is Kc or D of axis 0: as class ids + class values on a cls_gemv handle
+static void gemv_operand(const gpk_handle* h, GemvDesc& g) {
+  if (!h->cls_gemv || !(g.A == h->Kc[0] || g.A == h->D[0])) return;
+  const bool k = g.A == h->Kc[0];
+  g.cid = h->cls[0].cid;
+  g.cv = k ? h->cls[0].kval : h->cls[0].dval;
+  g.cdiag = k ? h->prob.jitter : 0.0;
+  g.ident = k ? 1 : 0;
+  g.A = nullptr;
+}
+
 static int enqueue_step_shard(gpk_handle* h, int apply);
 
 static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
@@ -452,6 +467,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
       GemvDesc q = g;
       q.A = A; q.x = x; q.y = y; q.alpha = alpha; q.C0 = C0; q.beta = beta; q.epi = epi; q.red = red;
       q.gate = gated ? h->pst[0] : nullptr;
+      gemv_operand(h, q);
       TRY(check_launch(launch_gemv(q, h->s), "gemv"));
       stamp(nm);
       return GPK_OK;
@@ -465,6 +481,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
       GemvDesc q = g;
       q.A = h->D[0]; q.x = h->alpha; q.y = h->R; q.epi = EPI_RESID; q.red = h->red_egap;
       q.red2 = h->red_quad; q.Q1 = h->Up; q.Q2 = h->alpha;
+      gemv_operand(h, q);
       TRY(check_launch(launch_gemv(q, h->s), "gemv"));
       stamp("gemv_resid");
     }
@@ -1521,6 +1538,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
       c.kval = kval; c.dval = dval; c.nchunk = nchunk; c.rb = rb; c.part = part;
     }
     h->bpa = std::max(pgrad_class_blocks(h->cls[0].ncls), L.dim == 2 ? pgrad_class_blocks(h->cls[1].ncls) : 0);
+    h->cls_gemv = h->chain_multi && L.dim == 1 && !(p->flags & GPK_FLAG_MATRIX_GEMV);
   } else {
     h->bpa = std::max(pgrad_blocks(L.n1), L.dim == 2 ? pgrad_blocks(L.n2) : 0);
   }
@@ -2124,6 +2142,7 @@ int gpk_predict(gpk_handle* h, const double* xte1, int32_t m1, const double* xte
       GemvDesc g{};
       g.A = A; g.lda = P1; g.x = x; g.y = y; g.p = P1; g.rows = rows; g.alpha = al;
       g.C0 = C0; g.beta = be; g.epi = EPI_STORE;
+      gemv_operand(h, g);
       (void)launch_gemv(g, h->s);
     };
     // alpha = K^{-1} u with one refinement step (matches solve() accuracy; 1d.py:176-179)
@@ -2330,6 +2349,7 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
       GemvDesc g{};
       g.A = h->D[0]; g.lda = P; g.x = h->alpha; g.y = tmp; g.p = P; g.rows = P; g.alpha = 1.0;
       g.epi = EPI_STORE;
+      gemv_operand(h, g);
       int rc = check_launch(launch_gemv(g, h->s), "gemv");
       if (rc) { cleanup(); return rc; }
       src = tmp;

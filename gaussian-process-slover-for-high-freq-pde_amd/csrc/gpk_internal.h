@@ -340,6 +340,11 @@ struct GemvDesc {
   double* red;       // per-block partials
   double* red2; const double* Q1; const double* Q2;  // per-block partials of sum Q1*Q2
   const double* gate; int ngate;
+  // class operand (cid != nullptr, A unused): A[i][j] = cv[cid[i*lda + j]], ident = 1 (K): + cdiag
+  // (the jitter) on i == j and the identity on pads (cid < 0); ident = 0 (D): zero on pads --
+  // bitwise the Kc / D matrices the inverse launch would have written, read as int32 ids (half
+  // the bytes)
+  const int* cid; const double* cv; double cdiag; int ident;
 };
 hipError_t launch_gemv(const GemvDesc& d, hipStream_t s);
 int gemv_blocks(int rows);

@@ -473,7 +473,7 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
       }
       if (!master) {
         if (F.Kc) F.Kc[o] = kv;
-        if (DERIV) F.D[o] = dv;
+        if (DERIV && F.D) F.D[o] = dv;
       }
       acc[r] = kv;
     } else {
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
       }
       if (write) {
         if (F.Kc) F.Kc[o] = kv;
-        if (DERIV) F.D[o] = dv;
+        if (DERIV && F.D) F.D[o] = dv;
       }
       return kv;
     }
@@ -749,7 +749,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
     for (int r = 0; r < 4; ++r) {
       const int i = I * 32 + 16 * wr + (lane >> 4) + 4 * r, j = J * 32 + 16 * wc + (lane & 15);
       acc[s][r] = kval_at(i, j, true);
-      if (GATHER && I != J) (void)kval_at(j, i, true);  // the mirrored Kc / D entries
+      if (GATHER && I != J && (F.Kc || (DERIV && F.D))) (void)kval_at(j, i, true);  // mirrored Kc / D
     }
   }
   const bool trm = t == 0 && m == 0;

@@ -120,6 +120,10 @@ typedef struct gpk_problem {
  * the small-factor path); NO_REFINE: none (explicit-inverse products only). */
 #define GPK_FLAG_REFINE_ALL 8192
 #define GPK_FLAG_NO_REFINE 16384
+/* Large 1D factors on the macro-tile chain: the inverse launch writes Kc and D as matrices and the
+ * GEMVs read them (round-2 form; default: the GEMVs read class ids + class values and the
+ * inverse writes neither). Bitwise the same results. */
+#define GPK_FLAG_MATRIX_GEMV 32768
 
 typedef struct gpk_handle gpk_handle;
 

@@ -109,6 +109,27 @@ def test_c2_multi_chain_matches_launch_per_sweep_path():
     assert rel(res[0][1], res[1][1]) < tol
 
 
+def test_c2_class_gemv_bitwise_equals_matrix_gemv():
+    """The GEMVs read Kc and D as class ids + class values (the inverse launch writes neither
+    matrix); GPK_FLAG_MATRIX_GEMV keeps the round-2 form.  Bitwise the same loss, gradient,
+    3-step trajectory, predictions and u_xx field."""
+    from gpk._lib import GPK_FLAG_MATRIX_GEMV
+    from gpk.problems import make_solver
+    xte = np.linspace(0.0, 1.0, 300)
+    out = []
+    for flags in (0, GPK_FLAG_MATRIX_GEMV):
+        s = make_solver("C2", seed=0, flags=flags)
+        try:
+            assert s.inverse_path() == "chain_multi"
+            loss, g = s.loss_grad()
+            losses = s.step(3)
+            out.append((loss, g, losses, s.get_flat(), s.predict(xte), s.forward_field("u_xx"), s.forward_field("K")))
+        finally:
+            s.close()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+
+
 def test_capped_capacity_falls_back_to_launch_per_sweep():
     from gpk.core import set_chain_capacity
     from gpk.problems import make_solver
