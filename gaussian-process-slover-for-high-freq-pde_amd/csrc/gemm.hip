@@ -766,6 +766,38 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvDesc d) {
     };
     double s[4] = {0.0, 0.0, 0.0, 0.0};
     int c = lane;
+    if ((n2 & 255) == 0) {
+      // whole 256-pair groups: up to 4 groups (16 pairs per lane) per batch -- every id load of
+      // the batch, then every value gather, then the FMAs in the loop below's order (two memory
+      // round trips per batch instead of two per group)
+      for (; c < n2; c += 1024) {
+        const int ng = min(4, (n2 - (c - lane)) >> 8);  // (uniform)
+        int2 iv[16];
+        double2 bv[16], av[16];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          if (g < ng)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              iv[4 * g + u] = ids[c + 256 * g + 64 * u];
+              bv[4 * g + u] = xv[c + 256 * g + 64 * u];
+            }
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          if (g < ng)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int col = 2 * (c + 256 * g + 64 * u);
+              av[4 * g + u] = make_double2(val(iv[4 * g + u].x, col), val(iv[4 * g + u].y, col + 1));
+            }
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          if (g < ng)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              s[u] = fma(av[4 * g + u].y, bv[4 * g + u].y, fma(av[4 * g + u].x, bv[4 * g + u].x, s[u]));
+      }
+    }
     for (; c + 192 < n2; c += 256) {
       int2 iv[4];
       double2 bv[4];

@@ -20,6 +20,7 @@
 #include <thread>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <string>
@@ -1526,7 +1527,8 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
       int *cid = nullptr, *cb = nullptr;
       // class-sum row chunks: <= 64 chunks of >= 16 rows (one 4-row group per wave and pass)
       const int n = a == 0 ? L.n1 : L.n2;
-      const int rb = std::max(16, (n + 63) / 64 + 15) / 16 * 16;
+      int rb = std::max(16, (n + 63) / 64 + 15) / 16 * 16;
+      if (const char* e = std::getenv("GPK_CSUM_RB")) rb = std::max(16, atoi(e) / 16 * 16);  // (experiment)
       const int nchunk = (n + rb - 1) / rb;
       A_(dist, U); A_(kval, U); A_(dval, U); A_(part, (size_t)2 * nchunk * U);
       A_(cid, (size_t)P * P); A_(cb, cbase[a].size());
@@ -2023,19 +2025,25 @@ int gpk_trace_reset(void) {
   trace_reset_spdinv();
   trace_reset_pgrad();
   trace_reset_gemm();
+  trace_reset_spdbig();
   return GPK_OK;
 }
 
 int gpk_trace_read(uint64_t* lo, uint64_t* hi, int32_t n) {
   if (!lo || !hi || n < TRACE_SLOTS) return fail(GPK_EINVAL, "need TRACE_SLOTS (256) slots");
-  uint64_t l[4][TRACE_SLOTS], h[4][TRACE_SLOTS];
+  uint64_t l[5][TRACE_SLOTS], h[5][TRACE_SLOTS];
   trace_fetch_assemble(l[0], h[0]);
   trace_fetch_spdinv(l[1], h[1]);
   trace_fetch_pgrad(l[2], h[2]);
   trace_fetch_gemm(l[3], h[3]);
+  trace_fetch_spdbig(l[4], h[4]);
   for (int i = 0; i < TRACE_SLOTS; ++i) {
-    lo[i] = std::min(std::min(l[0][i], l[3][i]), std::min(l[1][i], l[2][i]));
-    hi[i] = std::max(std::max(h[0][i], h[3][i]), std::max(h[1][i], h[2][i]));
+    lo[i] = l[0][i];
+    hi[i] = h[0][i];
+    for (int u = 1; u < 5; ++u) {
+      lo[i] = std::min(lo[i], l[u][i]);
+      hi[i] = std::max(hi[i], h[u][i]);
+    }
   }
 #ifdef GPK_TRACE
   return GPK_OK;

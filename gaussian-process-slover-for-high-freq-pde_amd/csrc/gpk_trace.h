@@ -36,7 +36,14 @@ enum TraceSlot {
   SLOT_MC_PUB = 192,    // the pass-0 tiles published (flags raised)
   SLOT_MC_DONE = 208,   // pass 1 done (end of the sweep)
   SLOT_MC_PROD = 224,   // pass-0 products done (before their stores)
+  // wide_update_kernel (spdinv_big.hip), sweep BIG_PROBE_SWEEP, factor 0: launch start (first
+  // workgroup), pivot workgroup [start, its tile done], pivot128 done, panel workgroups [first
+  // start, L^{-1} seen], panel done (last), tile workgroups' round 0 / 1 ends (max), quarter
+  // items [first start, last end]
+  SLOT_BIG_START = 240, SLOT_BIG_PIVTILE = 241, SLOT_BIG_PIVOT = 242, SLOT_BIG_PANEL_WAIT = 243,
+  SLOT_BIG_PANEL = 244, SLOT_BIG_ROUND0 = 245, SLOT_BIG_ROUND1 = 246, SLOT_BIG_QUARTER = 247,
 };
+constexpr int BIG_PROBE_SWEEP = 8;
 
 #ifdef GPK_TRACE
 #define GPK_TRACE_TU(tu)                                                                  \
@@ -81,5 +88,7 @@ void trace_fetch_pgrad(uint64_t* lo, uint64_t* hi);
 void trace_reset_pgrad();
 void trace_fetch_gemm(uint64_t* lo, uint64_t* hi);
 void trace_reset_gemm();
+void trace_fetch_spdbig(uint64_t* lo, uint64_t* hi);
+void trace_reset_spdbig();
 
 }  // namespace gpk

@@ -36,8 +36,11 @@
 #include "gemm_huge_dev.h"
 #include "gpk_internal.h"
 #include "spd_pivot.h"
+#include "gpk_trace.h"
 
 namespace gpk {
+
+GPK_TRACE_TU(spdbig)
 
 static std::atomic<int> g_big_wgs{0};  // spd_big_set_workgroups override (tests)
 void spd_big_set_workgroups(int g) { g_big_wgs.store(g > 0 ? g : 0); }
@@ -737,6 +740,8 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   // gx = tiles per factor slot.
   __shared__ double sm[WIDE_LDS];
   const int L = blockIdx.x;
+  const bool probe = k == BIG_PROBE_SWEEP && threadIdx.x == 0;  // (trace build only)
+  if (probe && L == 0) TR_LO(SLOT_BIG_START);
   if (L >= 8 * nx + 8) {  // the next sweep's panel (fused_panel)
     const int tmax = max(b.T[0], b.nmat > 1 ? b.T[1] : 0);
     const int pi = L - 8 * nx - 8;
@@ -745,16 +750,30 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     if (m >= b.nmat) return;
     const int T2 = (b.p[m] + WT - 1) / WT;
     if (k + 1 >= T2 || skip_pivot || pj >= 2 * b.T[m]) return;
-    fused_panel<2>(b, m, k, pj, (unsigned)(T2 - 1), sm);  // T2 - 1 panel-row tiles per sweep
+    // T2 - 1 panel-row tiles per sweep, counted in quarter tiles (a whole tile adds 4)
+    if (probe && m == 0) TR_LO(SLOT_BIG_PANEL_WAIT);
+    fused_panel<2>(b, m, k, pj, 4u * (unsigned)(T2 - 1), sm);
+    if (probe && m == 0) TR_HI(SLOT_BIG_PANEL);
     return;
   }
   const bool pivot = L >= first && L < first + 8;
   if (pivot && L - first >= b.nmat) return;
+  if (probe && pivot && L == first) TR_LO(SLOT_BIG_PIVTILE);
   const int tt = L < first ? L : L - 8;  // tile workgroup ordinal
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  // tile j of this workgroup -> (factor m, tile ti, tj); false past its run
-  auto tile_at = [&](int j, int& m, int& ti, int& tj) -> bool {
+  // Rounds: every XCD slot's run of per_xcd tiles is worked in rounds of nx tiles, so a last
+  // round of rem < nx tiles would leave most workgroups idle for a whole tile time (C5: 1056
+  // tiles on 496 workgroups = 2 rounds + 64 tiles).  When 4 rem <= nx, that last round is split
+  // into quarter tiles (64 x 64 outputs of the same 128-deep product; qq = quarter) worked by
+  // 4 rem workgroups at once: a quarter of a tile time.  Same MFMA sequence per output block:
+  // bitwise the whole-tile result.
+  const int full_rounds = per_xcd / nx, rem_tiles = per_xcd - full_rounds * nx;
+  const bool quarters = full_rounds >= 1 && rem_tiles > 0 && 4 * rem_tiles <= nx;
+  // item j of this workgroup -> (factor m, tile ti, tj, quarter qq: -1 = whole tile); false past
+  // its run
+  auto tile_at = [&](int j, int& m, int& ti, int& tj, int& qq) -> bool {
+    qq = -1;
     if (pivot) {
       if (j > 0) return false;
       m = L - first;
@@ -763,8 +782,16 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
       ti = tj = k + 1;
       return true;
     }
-    const int loc = (tt >> 3) + j * nx;
-    if (loc >= per_xcd) return false;
+    int loc;
+    if (quarters && j >= full_rounds) {
+      const int w = tt >> 3;
+      if (j > full_rounds || w >= 4 * rem_tiles) return false;
+      loc = full_rounds * nx + (w >> 2);
+      qq = w & 3;
+    } else {
+      loc = (tt >> 3) + j * nx;
+      if (loc >= per_xcd) return false;
+    }
     const int wi = (tt & 7) * per_xcd + loc;
     if (wi >= b.nmat * gx) return false;
     m = wi / gx;
@@ -783,10 +810,12 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   double* sA0 = sm;
   double* sB0 = sm + 2 * SZ;
   Regs R;
-  int m, ti, tj;
-  if (!tile_at(0, m, ti, tj)) return;
-  fetch<1, 0>(R, zbuf<2>(b, m, k), b.p[m], zbuf<2>(b, m, k), b.p[m], b.p[m], b.p[m], WT * ti, WT * tj, 0, t);
-  for (int j = 0;; ++j) {
+  int m, ti, tj, qq;
+  if (!tile_at(0, m, ti, tj, qq)) return;
+  int j = 0;
+  if (qq < 0)
+    fetch<1, 0>(R, zbuf<2>(b, m, k), b.p[m], zbuf<2>(b, m, k), b.p[m], b.p[m], b.p[m], WT * ti, WT * tj, 0, t);
+  for (; qq < 0; ++j) {
     const int p = b.p[m];
     const int T2 = (p + WT - 1) / WT;  // 128-tiles per dimension
     const bool has_next = k + 1 < T2;
@@ -798,9 +827,11 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     const int wK = min(WT, p - WT * k);  // sweep width (a multiple of 32)
     const bool inPi = ti == k, inPj = tj == k;
     const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
-    // the workgroup's next tile (its first K-step is fetched under this tile's last one)
-    int m2 = 0, ti2 = 0, tj2 = 0;
-    const bool more = tile_at(j + 1, m2, ti2, tj2);
+    // the workgroup's next tile (its first K-step is fetched under this tile's last one; a
+    // quarter item is fetched after the loop)
+    int m2 = 0, ti2 = 0, tj2 = 0, q2 = -1;
+    const bool next = tile_at(j + 1, m2, ti2, tj2, q2);
+    const bool more = next && q2 < 0;
     // The accumulators start at the tile's current values (zero base in the swept blocks;
     // clamped addresses: rows / columns past p are never stored) and the product is subtracted
     // (A operand staged negated): no separate base registers.  The base loads are issued right
@@ -867,17 +898,126 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     if (pivot) {
       // the next pivot block, factored in place from this workgroup's own stores (one L1 per
       // workgroup: visible after the barrier)
+      if (probe && m == 0) TR_HI(SLOT_BIG_PIVTILE);
       __syncthreads();
       const int r0 = WT * Q, w = min(WT, p - r0);
       pivot128(X + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 4 * Q, b.status[m], sm);
       release_add(b.flag[m] + 1, 1u);  // L^{-1} of pivot k + 1 ready (fused_panel)
+      if (probe && m == 0) TR_HI(SLOT_BIG_PIVOT);
       return;
     }
-    if (has_next && (ti == Q || tj == Q)) release_add(b.flag[m] + 2, 1u);  // next panel row
-    if (!more) return;
+    if (probe && j < 2) TR_HI(SLOT_BIG_ROUND0 + j);
+    if (has_next && (ti == Q || tj == Q)) release_add(b.flag[m] + 2, 4u);  // next panel row
+    if (!next) return;
     m = m2;
     ti = ti2;
     tj = tj2;
+    qq = q2;
+  }
+  // the quarter item (qq = 2 qi + qj): rows WT ti + 64 qi, columns WT tj + 64 qj; this wave's
+  // 32 x 32 block (wr, wc) as 2 x 2 MFMA blocks, 16-deep K-steps through the same double-buffered
+  // staging ([k][64] rows of Z at stride S)
+  {
+    __syncthreads();  // (the whole-tile loop's last reads of the staging buffers)
+    if (probe) TR_LO(SLOT_BIG_QUARTER);
+    const int p = b.p[m];
+    const int T2 = (p + WT - 1) / WT;
+    const bool has_next = k + 1 < T2;
+    const bool LAST = !has_next;
+    const int Q = k + 1;
+    double* X = b.X[m];
+    const double* Z = zbuf<2>(b, m, k);
+    const int i0 = WT * ti + 64 * (qq >> 1), j0 = WT * tj + 64 * (qq & 1);
+    const int wK = min(WT, p - WT * k);
+    const bool inPi = ti == k, inPj = tj == k;
+    const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
+    const int li = lane & 15, lk = lane >> 4;
+    d4 acc[2][2];
+    {
+      const double f = (inPi || inPj) ? 0.0 : 1.0;
+#pragma unroll
+      for (int bx = 0; bx < 2; ++bx)
+#pragma unroll
+        for (int by = 0; by < 2; ++by)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = min(i0 + 32 * wr + 16 * bx + lk + 4 * r, p - 1);
+            const int col = min(j0 + 32 * wc + 16 * by + li, p - 1);
+            acc[bx][by][r] = X[(size_t)row * p + col] * f;
+          }
+    }
+    // K-step kt: Z[16 kt + kr][i0 + c] (A, negated) and Z[16 kt + kr][j0 + c] (B), kr < 16,
+    // c < 64: two 16-B loads per operand and thread, 512 B per k row (coalesced); the next
+    // K-step's loads in flight under the current one's MFMAs.  (All K-steps' loads up front --
+    // one round trip per item -- measured slower: 121 vs 113 us per update launch.)
+    auto qfetch = [&](double2 (&ra)[2], double2 (&rb)[2], int k0) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int e = t + 256 * q, kr = e >> 5, c = 2 * (e & 31);
+        ra[q] = ld2(Z + (size_t)(k0 + kr) * p + min(i0 + c, p - 2));
+        rb[q] = ld2(Z + (size_t)(k0 + kr) * p + min(j0 + c, p - 2));
+      }
+    };
+    auto qstore = [&](const double2 (&ra)[2], const double2 (&rb)[2], double* sA, double* sB) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int e = t + 256 * q, kr = e >> 5, c = 2 * (e & 31);
+        *reinterpret_cast<double2*>(sA + kr * S + c) = make_double2(-ra[q].x, -ra[q].y);
+        *reinterpret_cast<double2*>(sB + kr * S + c) = rb[q];
+      }
+    };
+    const int nk = wK / KS;
+    double2 ra[2], rb[2];
+    qfetch(ra, rb, 0);
+    qstore(ra, rb, sA0, sB0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) qfetch(ra, rb, (kt + 1) * KS);
+      const double* sA = sA0 + cur * SZ;
+      const double* sB = sB0 + cur * SZ;
+#pragma unroll
+      for (int kk = 0; kk < KS / 4; ++kk) {
+        const int kr = 4 * kk + lk;
+        double a[2], bb[2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          a[x] = sA[kr * S + 32 * wr + 16 * x + li];
+          bb[x] = sB[kr * S + 32 * wc + 16 * x + li];
+        }
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y)
+            acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], bb[y], acc[x][y], 0, 0, 0);
+      }
+      if (kt + 1 < nk) qstore(ra, rb, sA0 + (cur ^ 1) * SZ, sB0 + (cur ^ 1) * SZ);
+      __syncthreads();
+    }
+    double mx = 0.0;
+#pragma unroll
+    for (int bx = 0; bx < 2; ++bx)
+#pragma unroll
+      for (int by = 0; by < 2; ++by)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i0 + 32 * wr + 16 * bx + lk + 4 * r;
+          const int col = j0 + 32 * wc + 16 * by + li;
+          if (row < p && col < p) {
+            const double v = sgn * acc[bx][by][r];
+            X[(size_t)row * p + col] = v;
+            if (LAST && row == col && row < b.n[m]) mx = fmax(mx, v);
+          }
+        }
+    if (LAST && ti == tj) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+      if (lane == 0 && mx > 0.0)
+        atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
+                  (unsigned long long)__double_as_longlong(mx));
+    }
+    if (has_next && (ti == Q || tj == Q)) release_add(b.flag[m] + 2, 1u);  // a quarter of a row tile
+    if (probe) TR_HI(SLOT_BIG_QUARTER);
   }
 }
 
