@@ -1525,10 +1525,12 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
       ClassArgs& c = h->cls[a];
       double *dist = nullptr, *kval = nullptr, *dval = nullptr, *part = nullptr;
       int *cid = nullptr, *cb = nullptr;
-      // class-sum row chunks: <= 64 chunks of >= 16 rows (one 4-row group per wave and pass)
+      // class-sum row chunks: <= 64 chunks of >= 16 rows (one 4-row group per wave and pass);
+      // with the LDS bins (> 8 variants per diagonal: 70 KB per workgroup, two per CU) <= 32
+      // chunks -- C2: 0.693 -> 0.688 ms/step (64 rows; 128 the same, 256 slower)
       const int n = a == 0 ? L.n1 : L.n2;
-      int rb = std::max(16, (n + 63) / 64 + 15) / 16 * 16;
-      if (const char* e = std::getenv("GPK_CSUM_RB")) rb = std::max(16, atoi(e) / 16 * 16);  // (experiment)
+      const int maxchunks = vmax[a] > 8 ? 32 : 64;
+      const int rb = std::max(16, (n + maxchunks - 1) / maxchunks + 15) / 16 * 16;
       const int nchunk = (n + rb - 1) / rb;
       A_(dist, U); A_(kval, U); A_(dval, U); A_(part, (size_t)2 * nchunk * U);
       A_(cid, (size_t)P * P); A_(cb, cbase[a].size());

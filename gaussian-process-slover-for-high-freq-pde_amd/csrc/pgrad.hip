@@ -188,39 +188,65 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
   // exec-masked branch behind a vmcnt(0) wait).
   // (4 rows per wave and pass, 8 pairs; 8 rows -- twice the loads per round trip -- measured
   // slower with the LDS bins: C2 30 -> 32 us, C4 3.5 -> 4.5 us)
-  constexpr int RP = 4, NP = 2 * RP;
+  // 1D (MODE1D): K^{-1} is symmetric (its upper triangle mirrors the lower one) and so are the
+  // class ids, so a class's pairs (i, j) and (j, i) are folded into one lower pair:
+  // G_K(i,j) + G_K(j,i) = c K^{-1}_ij - a_i a_j - v (b_i a_j + b_j a_i), G_D likewise -- half the
+  // loads and bin updates; 8 rows per wave and pass, 8 lower pairs.
+  static_assert(!(MODE1D && DERIV == 1), "the 1D fold assumes a symmetric G_D sign");
+  constexpr int RP = MODE1D ? 8 : 4, NP = 8;
   for (int base = r0; base < r1; base += 4 * RP) {
     int ii[NP], jj[NP], msk[NP];
+    if (MODE1D) {
 #pragma unroll
-    for (int s = 0; s < RP; ++s) {
-      const int r = base + w + 4 * s;
-      const bool in = kv && r < r1;
-      const bool lo = in && r >= k, up = in && k > 0 && r + k < n;
-      ii[2 * s] = lo ? r : 0;
-      jj[2 * s] = lo ? r - k : 0;
-      msk[2 * s] = -(int)lo;
-      ii[2 * s + 1] = up ? r : 0;
-      jj[2 * s + 1] = up ? r + k : 0;
-      msk[2 * s + 1] = -(int)up;
+      for (int s = 0; s < NP; ++s) {
+        const int r = base + w + 4 * s;
+        const bool lo = kv && r < r1 && r >= k;
+        ii[s] = lo ? r : 0;
+        jj[s] = lo ? r - k : 0;
+        msk[s] = -(int)lo;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < RP; ++s) {
+        const int r = base + w + 4 * s;
+        const bool in = kv && r < r1;
+        const bool lo = in && r >= k, up = in && k > 0 && r + k < n;
+        ii[2 * s] = lo ? r : 0;
+        jj[2 * s] = lo ? r - k : 0;
+        msk[2 * s] = -(int)lo;
+        ii[2 * s + 1] = up ? r : 0;
+        jj[2 * s + 1] = up ? r + k : 0;
+        msk[2 * s + 1] = -(int)up;
+      }
     }
     int cv[NP];
     double g0[NP], g1[NP];
 #pragma unroll
     for (int s = 0; s < NP; ++s) cv[s] = C.cid[(size_t)ii[s] * p + jj[s]];
     if (MODE1D) {  // G_K = c/2 K^{-1} - 1/2 alpha alpha^T - v beta alpha^T, G_D = v R alpha^T
-      double ai[NP], aj[NP], bi[NP], ri[NP];
+      double ai[NP], aj[NP], bi[NP], bj[NP], ri[NP], rj[NP];
 #pragma unroll
       for (int s = 0; s < NP; ++s) {
         g0[s] = A.Kinv[(size_t)ii[s] * p + jj[s]];
         ai[s] = A.alpha[ii[s]];
         aj[s] = A.alpha[jj[s]];
         bi[s] = A.beta[ii[s]];
+        bj[s] = A.beta[jj[s]];
         ri[s] = A.R[ii[s]];
+        rj[s] = A.R[jj[s]];
       }
+      if (k == 0) {  // the diagonal: one pair
 #pragma unroll
-      for (int s = 0; s < NP; ++s) {
-        g1[s] = vs * ri[s] * aj[s];
-        g0[s] = hc * g0[s] - 0.5 * ai[s] * aj[s] - vs * bi[s] * aj[s];
+        for (int s = 0; s < NP; ++s) {
+          g1[s] = vs * ri[s] * aj[s];
+          g0[s] = hc * g0[s] - 0.5 * ai[s] * aj[s] - vs * bi[s] * aj[s];
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < NP; ++s) {
+          g1[s] = vs * (ri[s] * aj[s] + rj[s] * ai[s]);
+          g0[s] = 2.0 * hc * g0[s] - ai[s] * aj[s] - vs * (bi[s] * aj[s] + bj[s] * ai[s]);
+        }
       }
     } else {
 #pragma unroll
