@@ -146,6 +146,10 @@ def large_factors(steps=3):
         n = 4096
         tus, tfl, _ = s.bench_kernel("spd_tiles", 3)
         gus, _, gby = s.bench_kernel("gather", 5)
+        # the same launch inside whole steps (stage 'assemble' = class_eval + the gather, HIP
+        # events around the stage): the first gather after a step's GEMMs runs ~2x slower than
+        # back to back, so both are reported
+        stages = s.profile_stages(3)
         path = s.inverse_path()
     finally:
         s.close()
@@ -159,7 +163,12 @@ def large_factors(steps=3):
             # factors from the class values and reads each element's class id (bytes it moves)
             "assembly": {"kernel": "gather_wide_kernel (K, Kc, D of both factors from class values, nontemporal stores)",
                          "us": gus, "bytes": gby, "hbm_gbs": gby / (gus * 1e-6) / 1e9,
-                         "hbm_frac": gby / (gus * 1e-6) / 1e9 / PEAK_HBM_GBS}}
+                         "hbm_frac": gby / (gus * 1e-6) / 1e9 / PEAK_HBM_GBS,
+                         "timing": "back to back, HIP events",
+                         "in_step": {"stage": "assemble (class_eval + gather)",
+                                     "us": stages.get("assemble"),
+                                     "hbm_gbs": gby / (stages["assemble"] * 1e-6) / 1e9
+                                     if stages.get("assemble") else None}}}
 
 
 def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
@@ -314,6 +323,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--step1-calls", type=int, default=200)
+    ap.add_argument("--no-prepare-warmup", action="store_true",
+                    help="run the warm-up steps without a prepared whole-call graph (A/B)")
     ap.add_argument("--no-large", action="store_true", help="skip the C5-size MFMA section")
     ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the row-sharded section")
     ap.add_argument("--sharded-steps", type=int, default=50)
@@ -340,6 +351,8 @@ def main():
     cfg = CONFIGS[a.config]
     s = _DryRunSolver(rank) if a.dry_run else make_solver(a.config, seed=rank, device=local)
     s.prepare(a.steps)                   # every graph the timed call can launch, built untimed
+    if a.warmup > 1 and not a.no_prepare_warmup:
+        s.prepare(a.warmup)              # ... and the warm-up call's (one graph launch, not W)
     s.step(a.warmup)                     # warm-up steps
     s.sync()
     replicas.barrier(ctx)

@@ -2,7 +2,7 @@
 # Round-3 measurement session: GPU suite (parity log), smoke, the driver-shape bench line, and
 # rocprofv3 traces + PMC passes (HBM FETCH/WRITE, fp64 MFMA) for C4 (bench), C5 and C2.
 set -o pipefail
-OUT=gpurun_out/r3p
+OUT=${OUT:-gpurun_out/r3p}
 mkdir -p $OUT
 export TMPDIR=/tmp
 export GPK_PARITY_LOG=$OUT/parity.jsonl
