@@ -100,3 +100,4 @@ def test_c4_size_class_counts():
     s = device_solver(prob, 30, fs)
     assert s.class_counts() == [1297, 1297]
     s.close()
+
