@@ -588,7 +588,7 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(GemmBatch batch, const St
 // Largest-size variant (M, N >= ~2048, e.g. the 4096^2 advection grid): a 128x128 output tile
 // per 256-thread workgroup, each wave a 64x64 quadrant = 4x4 v_mfma_f64_16x16x4 blocks (every
 // LDS fragment feeds 4 MFMAs, 16 independent accumulation chains per wave); 16-deep K-steps
-// through double-buffered LDS ([k][m] / [k][n], rows 144 doubles apart = 32 banks), the next
+// through double-buffered LDS ([k][m] / [k][n], rows 140 doubles apart: gemm_huge_dev.h), the next
 // step prefetched global -> registers with 16-B loads that read whole contiguous segments.
 // A dual product is folded into the same accumulators: its A2 operand is scaled by
 // alpha2 / alpha on the way into LDS, and the epilogue applies alpha once.  Tiles are dealt

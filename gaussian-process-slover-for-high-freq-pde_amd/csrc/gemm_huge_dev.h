@@ -2,9 +2,14 @@
 // (gemm.hip gemm_huge_kernel) and the large-factor SPD inverse's update (spdinv_big.hip).
 // A 128x128 output tile per 256-thread workgroup, each wave a 64x64 quadrant = 4x4
 // v_mfma_f64_16x16x4 blocks (every LDS fragment feeds 4 MFMAs, 16 independent accumulation
-// chains per wave); 16-deep K-steps through double-buffered LDS ([k][m] / [k][n], rows 144
-// doubles apart = 32 banks), the next step prefetched global -> registers with 16-B loads that
-// read whole contiguous segments.  LDS: 2 x 2 x KS x S doubles (72 KB).
+// chains per wave); 16-deep K-steps through double-buffered LDS ([k][m] / [k][n], rows S = 140
+// doubles apart), the next step prefetched global -> registers with 16-B loads that read whole
+// contiguous segments.  LDS: 2 x 2 x KS x S doubles (70 KB).
+// Row stride: a k-contiguous operand (A[i][k], B[j][k]) is transposed into LDS by 8-B stores,
+// 8 k rows x 8 m columns per wave instruction; with S = 144 (a multiple of 16 doubles) the 8 k
+// rows hit the same banks (8-way), with S = 140 (or 148, 156: S = 4 or 12 mod 16) they spread.
+// C5 gemm_B stage 60.0 -> 63.6 TF/s, C5 step 43.0 -> 41.2 ms (same box; 152: 60.0, 164: 52.2
+// -- one workgroup per CU).
 #pragma once
 #include "gpk_internal.h"
 
@@ -13,7 +18,7 @@ namespace gpk {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 namespace huge {
-constexpr int TM = 128, KS = 16, S = 144, GROUP_M = 4;
+constexpr int TM = 128, KS = 16, S = 140, GROUP_M = 4;
 
 struct Regs { double2 a[4], b[4]; };
 
