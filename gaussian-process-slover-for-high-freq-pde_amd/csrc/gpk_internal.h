@@ -171,6 +171,7 @@ struct SpdArgs {
   int* status;     // nonzero => not positive definite
   unsigned int* flag;  // large path: [3] hand-off / pivot-done / panel-row counters
   int wide;        // large path: 128-wide sweeps (else 64)
+  int no_quarters; // 128-wide update: keep the last round in whole tiles (tests, GPK_FLAG_NO_QUARTER_TILES)
   double* Z;       // large path: double-buffered panel [2][128][p] (nullable: Y)
 };
 // Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.

@@ -62,6 +62,7 @@ struct BigSpdBatch {
   int p[2], n[2], T[2];  // T: 64-wide tiles per dimension
   int G;                 // tile workgroups per factor in the update launch
   int nmat;
+  int no_quarters;       // (SpdArgs::no_quarters)
 };
 
 __device__ __forceinline__ int bw(int p, int I) { return min(BW, p - BW * I); }
@@ -769,7 +770,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   // 4 rem workgroups at once: a quarter of a tile time.  Same MFMA sequence per output block:
   // bitwise the whole-tile result.
   const int full_rounds = per_xcd / nx, rem_tiles = per_xcd - full_rounds * nx;
-  const bool quarters = full_rounds >= 1 && rem_tiles > 0 && 4 * rem_tiles <= nx;
+  const bool quarters = !b.no_quarters && full_rounds >= 1 && rem_tiles > 0 && 4 * rem_tiles <= nx;
   // item j of this workgroup -> (factor m, tile ti, tj, quarter qq: -1 = whole tile); false past
   // its run
   auto tile_at = [&](int j, int& m, int& ti, int& tj, int& qq) -> bool {
@@ -1050,6 +1051,7 @@ BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   // Measured at 2048: 1177 us per inverse vs 1243 us with 383 or 511
   b.G = g_big_wgs.load() > 0 ? g_big_wgs.load() : 255;
   b.nmat = nmat;
+  b.no_quarters = a[0].no_quarters;
   for (int m = 0; m < nmat; ++m) {
     b.X[m] = a[m].X; b.Z[m] = a[m].Z ? a[m].Z : a[m].Y; b.Li[m] = a[m].piv;
     b.ldet[m] = a[m].ldet; b.pst[m] = a[m].pst; b.status[m] = a[m].status; b.flag[m] = a[m].flag;

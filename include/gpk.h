@@ -124,6 +124,9 @@ typedef struct gpk_problem {
  * GEMVs read them (round-2 form; default: the GEMVs read class ids + class values and the
  * inverse writes neither). Bitwise the same results. */
 #define GPK_FLAG_MATRIX_GEMV 32768
+/* 128-wide SPD inverse: keep the update's last round of tiles whole (default: quarter tiles when
+ * that round would leave most workgroups idle). Bitwise the same results. */
+#define GPK_FLAG_NO_QUARTER_TILES 65536
 
 typedef struct gpk_handle gpk_handle;
 

@@ -156,3 +156,31 @@ def test_rank_group_never_uses_the_chain():
         assert g.inverse_path() == "sweep"
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("n1,n2", [(3072, 3072), (4096, 4096)])
+def test_wide_inverse_quarter_tiles_bitwise_whole_tiles(n1, n2):
+    """The 128-wide update works its last round of tiles as quarter tiles when that round would
+    leave most workgroups idle (C5 size: 64 of 1056 tiles; 3072^2: 24 of 600); each output
+    block sees the same MFMA sequence, so the loss, gradient and a 2-step trajectory are bitwise
+    those of whole tiles (GPK_FLAG_NO_QUARTER_TILES)."""
+    from gpk._lib import GPK_FLAG_NO_QUARTER_TILES
+    from gpk.problems import make_solver
+    out = []
+    for flags in (0, GPK_FLAG_NO_QUARTER_TILES):
+        if n1 == 4096:
+            s = make_solver("C5", seed=0, flags=flags)
+        else:
+            prob, params, _, fs = problem_2d(eq="advection", n1=n1, n2=n2, Q=6, seed=3)
+            s = device_solver(prob, 6, fs, flags=flags)
+            s.set_params(params)
+        try:
+            assert s.inverse_path() == "big_wide"
+            loss, g = s.loss_grad()
+            losses = s.step(2)
+            s.sync()
+            out.append((loss, g, losses, s.get_flat()))
+        finally:
+            s.close()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
