@@ -181,3 +181,23 @@ def test_step_returns_on_report_and_later_calls_are_ordered():
     finally:
         a.close()
         b.close()
+
+
+def test_many_single_step_calls_bitwise_one_long_call():
+    """500 step(1) calls (each returning on its report's ready word while the device still runs
+    the previous call's tail) against one step(500) call (prepared 64-step chunks + remainder):
+    bitwise the same losses and final state."""
+    from gpk.problems import make_solver
+    a = make_solver("C4", seed=1)
+    b = make_solver("C4", seed=1)
+    try:
+        la = np.concatenate([a.step(1) for _ in range(500)])
+        b.prepare(500)
+        lb = b.step(500)
+        assert np.array_equal(la, lb)
+        for x, y in zip(_state(a), _state(b)):
+            assert np.array_equal(x, y)
+        assert a.graph_mode()[1] == b.graph_mode()[1]  # same rollbacks
+    finally:
+        a.close()
+        b.close()
