@@ -17,6 +17,8 @@ enum TraceSlot {
   SLOT_SWEEP = 4,         // + k (k < 16): whole sweep launch k
   SLOT_SWEEP_PIVOT = 20,  // + k: the next-pivot factorisation inside sweep k
   SLOT_PREFETCH_MISS = 36,  // chain, factor 0: first / last pivot whose inputs missed the prefetch
+  SLOT_PG_GARR = 37,        // pgrad tail: a group's last block arrived (first / last group)
+  SLOT_PG_ULAST = 38,       // pgrad U plane: the last U workgroup done
   SLOT_CLASS_SUM = 40, SLOT_PGRAD = 41, SLOT_PG_CONTRACT = 42, SLOT_PG_GROUP = 43,
   SLOT_PG_TOP = 44, SLOT_PG_UPLANE = 45, SLOT_PG_FINAL = 46,
   // dispatch spread (last workgroup start) and intermediate points

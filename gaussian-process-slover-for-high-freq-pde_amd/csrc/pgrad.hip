@@ -102,6 +102,10 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
   if (t == 0 && blk == 0 && axis == 0) TR_HI(SLOT_PG_CONTRACT);
   if (t == 0 && blk == b.bpa - 1 && axis == b.naxes - 1) TR_HI(SLOT_PG_START);
   if (!arrive_last(T.gcount + axis * T.ngpa + gi, (unsigned)gsize, &s_last)) return;
+  if (t == 0) {
+    TR_LO(SLOT_PG_GARR);
+    TR_HI(SLOT_PG_GARR);
+  }
   const double* part = b.ax[axis].part;
   for (int x = t; x < 3 * QMAX; x += 256) {
     double acc = 0.0;
@@ -367,6 +371,7 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
     const int nu = tail_nu(b.tail.adam.L);
     for (int e = blk * 256 + threadIdx.x; e < nu; e += gridDim.x * 256) adam_u_elem(b.tail.adam, e);
     if (threadIdx.x == 0 && blk == 0) TR_HI(SLOT_PG_UPLANE);
+    if (threadIdx.x == 0 && blk == gridDim.x - 1) TR_HI(SLOT_PG_ULAST);
     return;
   }
   if (blk >= b.bpa) return;  // the U plane is wider than the gradient planes

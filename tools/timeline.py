@@ -25,7 +25,8 @@ NAMES = {0: "class_eval first wg", 1: "gather pivot wg | chain wg(0,0)", 2: "piv
          54: "chain: factor-1 pivot chain done", 55: "fin: loads issued", 56: "fin: sums done",
          57: "fin: loss done", 58: "chain last sweep: L flag seen", 59: "chain last sweep: L in LDS",
          60: "chain last sweep: products done", 61: "chain last sweep: tile out + done",
-         62: "chain last sweep: aug tile out + done", 36: "chain: prefetch missed (first..last)"}
+         62: "chain last sweep: aug tile out + done", 36: "chain: prefetch missed (first..last)",
+         37: "pg group complete (first..last)", 38: "pg U plane last wg"}
 for k in range(16):
     NAMES[64 + 4 * k] = f"gemm stage {k} first wg"
     NAMES[65 + 4 * k] = f"  gemm {k} first wg loaded"
