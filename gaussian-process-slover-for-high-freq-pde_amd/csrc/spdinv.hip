@@ -608,14 +608,15 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
 
 // ---- multi-tile chain: large factors (1D, p up to 2048) -------------------------------------
 // chain_kernel owns one 32x32 tile per workgroup (T^2 workgroups: p <= ~700).  Here a workgroup
-// owns a LOWER macro tile -- rows {2R, 2R+1} x one pair of 32-column tiles {2C, 2C+1}, C < R - 1,
-// or, as the last workgroup of macro row R, the pair {2R-2, 2R-1} together with the diagonal
-// 2x2 block (its three lower tiles) -- so p = 2048 needs 1 + 32*31/2 = 497 workgroups + the
-// pivot chain (two per CU).  The pivot chain is chain_kernel's (chain_master); per sweep k a
+// owns a LOWER macro tile -- rows {2R, 2R+1} x one pair of 32-column tiles {2C, 2C+1}, C < R --
+// and up to one tile of its macro row's diagonal 2x2 block (multi_role: the three lower tiles
+// go to three different workgroups of the row from R = 3 on, so no workgroup updates more than
+// five tiles per sweep) -- so p = 2048 needs 1 + 32*31/2 = 497 workgroups + the pivot chain
+// (two per CU).  The pivot chain is chain_kernel's (chain_master); per sweep k a
 // tile workgroup:
 //   * waits for the panel tiles of its row / column pairs and L_k^{-1}, loads them (sc1);
 //   * forms V = L_k^{-1} X_{k,.} for its (up to) four tile rows / columns (MFMA, LDS);
-//   * updates its (up to) seven tiles with chain_kernel's operations -- first the tiles that
+//   * updates its (up to) five tiles (seven in macro row 1) with chain_kernel's operations -- first the tiles that
 //     feed the next sweep's panel or the pivot chain, published together (one drain + barrier),
 //     then the rest.
 // Storage is the lower triangle: panel slot (k, J) of PB holds X_{k,J} after sweep k-1; for J > k
@@ -639,7 +640,7 @@ __device__ __forceinline__ d4 mma_f(FA fa, FB fb, int wr, int wc, int lane, d4 a
 
 // slot s of a macro-tile workgroup: s < 4 the column pair c0 (rows 2R + (s >> 1), column
 // 2 c0 + (s & 1)), s = 4..6 the diagonal block (2R,2R), (2R+1,2R), (2R+1,2R+1)
-__device__ __forceinline__ void multi_slot(int s, int R, int c0, int& I, int& J) {
+__host__ __device__ inline void multi_slot(int s, int R, int c0, int& I, int& J) {
   if (s < 4) {
     I = 2 * R + (s >> 1);
     J = 2 * c0 + (s & 1);
@@ -649,19 +650,25 @@ __device__ __forceinline__ void multi_slot(int s, int R, int c0, int& I, int& J)
   }
 }
 
-// macro-tile workgroup g (0-based) -> macro row R, its column pair c0 (plain part; -1: none) and
-// whether it holds the diagonal block.  Row 0: the diagonal block only; row R >= 1: R - 1 plain
-// workgroups (c0 = 0 .. R-2), then the merged one (c0 = R-1 + diagonal).
-__host__ __device__ inline void multi_role(int g, int& R, int& c0, bool& diag) {
+// macro-tile workgroup g (0-based) -> macro row R, its column pair c0 (-1: none) and the tiles of
+// the diagonal 2x2 block it holds (dmask bit s - 4 for slot s).  Row 0: the diagonal block only;
+// row R >= 1: R workgroups c0 = 0 .. R-1.  The pivot chain's inputs after sweep k are tiles
+// (k+2, k+1) and (k+2, k+2), and every workgroup updates all of its tiles in every sweep, so the
+// workgroup holding an input tile must not be slowed by extra tiles: (2R+1, 2R+1) goes to c0 =
+// R-1, (2R, 2R) to R-2 and (2R+1, 2R) to R-3 (rows 1, 2: to c0 = 0 where those do not exist).
+// Round 2's form gave the whole block to c0 = R-1: seven tiles, four of them in the critical
+// pass of sweep 2R-1, which set the C2 sweep cycle.
+__host__ __device__ inline void multi_role(int g, int& R, int& c0, int& dmask) {
   if (g == 0) {
-    R = 0; c0 = -1; diag = true;
+    R = 0; c0 = -1; dmask = 7;
     return;
   }
   int r = 1, first = 1;  // first workgroup of macro row r: 1 + r(r-1)/2
   while (first + r <= g) { first += r; ++r; }
   R = r;
   c0 = g - first;
-  diag = c0 == r - 1;
+  const int o4 = r >= 2 ? r - 2 : 0, o5 = r >= 3 ? r - 3 : 0, o6 = r - 1;
+  dmask = (c0 == o4 ? 1 : 0) | (c0 == o5 ? 2 : 0) | (c0 == o6 ? 4 : 0);
 }
 
 __host__ __device__ inline int multi_workgroups(int T) {  // per factor, + the pivot chain
@@ -685,9 +692,8 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
   // pass over the CUs does not double up), the tile workgroups around it
   const int mpos = b.mpos < nwg ? b.mpos : 0;
   const bool master = (int)blockIdx.x == mpos;
-  int R = 0, c0 = -1;
-  bool hasdiag = false;
-  if (!master) multi_role((int)blockIdx.x - ((int)blockIdx.x > mpos ? 1 : 0), R, c0, hasdiag);
+  int R = 0, c0 = -1, dmask = 0;
+  if (!master) multi_role((int)blockIdx.x - ((int)blockIdx.x > mpos ? 1 : 0), R, c0, dmask);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int tx = t & 31, ty = t >> 5;
@@ -710,7 +716,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
   auto valid = [&](int s) {
     if (master) return false;
     if (s < 4 && c0 < 0) return false;
-    if (s >= 4 && !hasdiag) return false;
+    if (s >= 4 && !((dmask >> (s - 4)) & 1)) return false;
     int I, J;
     multi_slot(s, R, c0, I, J);
     return I < T && J <= I;
@@ -840,7 +846,8 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
   auto vslot_of_col = [&](int s) { return s < 4 ? 2 + (s & 1) : (s == 6 ? 1 : 0); };
   for (int k = 0; k < T && !master; ++k) {
     // probes (gpk_trace.h SLOT_MC_*): the workgroup owning tile (k+2, k+2), factor 0
-    const bool trc = t == 0 && m == 0 && hasdiag && k < 16 && (k + 2 == 2 * R || k + 2 == 2 * R + 1);
+    const bool trc = t == 0 && m == 0 && k < 16 &&
+                     ((k + 2 == 2 * R && (dmask & 1)) || (k + 2 == 2 * R + 1 && (dmask & 4)));
     // issue priority: the sweep's front half (loads, V, the pass-0 tiles that feed sweep k+1 and
     // the pivot chain) over the pass-1 products of the workgroup sharing this CU
     __builtin_amdgcn_s_setprio(2);
@@ -971,7 +978,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
       else if (row == col && I * 32 + row < F.n) mx = fmax(mx, y);
     }
   }
-  if (hasdiag) {
+  if (dmask & 5) {  // holds a diagonal tile
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
     if (lane == 0 && mx > 0.0)

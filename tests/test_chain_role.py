@@ -54,3 +54,57 @@ def test_chain_role_is_a_bijection(tmp_path):
     subprocess.run(["g++", "-O1", "-std=c++17", str(cpp), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.strip()
     assert out == "0"
+
+
+SPD = os.path.join(os.path.dirname(HDR), "spdinv.hip")
+
+MULTI_MAIN = r"""
+#include <cstdio>
+#include <vector>
+#include <algorithm>
+int main() {
+  int bad = 0;
+  for (int T = 1; T <= 80; ++T) {
+    const int MT = (T + 1) / 2, nwg = 1 + MT * (MT - 1) / 2;
+    std::vector<int> own(T * T, 0);
+    for (int g = 0; g < nwg; ++g) {
+      int R, c0, dm, n = 0;
+      multi_role(g, R, c0, dm);
+      for (int s = 0; s < 7; ++s) {
+        if (s < 4 && c0 < 0) continue;
+        if (s >= 4 && !((dm >> (s - 4)) & 1)) continue;
+        int I, J;
+        multi_slot(s, R, c0, I, J);
+        if (I >= T || J > I) continue;
+        ++own[I * T + J];
+        ++n;
+      }
+      if (R >= 3 && n > 5) ++bad;   // no workgroup past macro row 2 updates more than 5 tiles
+      if (R == 2 && n > 6) ++bad;
+    }
+    for (int I = 0; I < T; ++I)
+      for (int J = 0; J < T; ++J) bad += own[I * T + J] != (J <= I ? 1 : 0);
+  }
+  std::printf("%d\n", bad);
+  return 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_multi_role_covers_lower_triangle(tmp_path):
+    """chain_multi_kernel's workgroup -> tiles map (spdinv.hip multi_role / multi_slot): every
+    lower tile of a T x T factor has exactly one owner, and the diagonal block's tiles are spread
+    so that no workgroup from macro row 3 on holds more than five tiles."""
+    src = open(SPD).read()
+    fns = []
+    for name in ("multi_slot", "multi_role"):
+        m = re.search(r"__host__ __device__ inline void " + name + r"\(.*?\n}\n", src, re.S)
+        assert m, name + " not found in spdinv.hip"
+        fns.append(m.group(0).replace("__host__ __device__ ", ""))
+    cpp = tmp_path / "multi.cpp"
+    cpp.write_text("\n".join(fns) + MULTI_MAIN)
+    exe = tmp_path / "multi"
+    subprocess.run(["g++", "-O1", "-std=c++17", str(cpp), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.strip()
+    assert out == "0"
