@@ -1166,7 +1166,7 @@ static int reset_handoffs(gpk_handle* h) {
     const size_t P = a == 0 ? L.p1 : L.p2, T = P / 32;
     const size_t nflags = T * (T + (L.p1 + L.p2) / 32) + 2 * T + 1;
     HIPCHK(hipMemsetD32Async(h->cgran[a], CHAIN_SENTINEL32, T * 4096, h->s));
-    if (h->PB2[a]) HIPCHK(hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * P * P, h->s));
+    if (h->PB2[a]) HIPCHK(hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * multi_half((int)P), h->s));
     if (h->cepoch[a]) HIPCHK(hipMemsetAsync(h->cepoch[a], 0, 4 * sizeof(unsigned int), h->s));
     HIPCHK(hipMemsetAsync(h->cflags[a], 0, nflags * sizeof(unsigned int), h->s));
     HIPCHK(hipMemsetAsync(h->aflag[a], 0, 4 * sizeof(unsigned int), h->s));
@@ -1484,9 +1484,9 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     if (hipMemsetD32Async(h->cgran[a], CHAIN_SENTINEL32, (size_t)(P / 32) * 4096, h->s) != hipSuccess)
       return bail(fail(GPK_EHIP, "initialise the pivot-chain input slots"));
     if (h->chain_multi) {
-      A_(h->PB2[a], (size_t)2 * P * P);
+      A_(h->PB2[a], 2 * multi_half(P));
       A_(h->cepoch[a], 4);
-      if (hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, (size_t)4 * P * P, h->s) != hipSuccess)
+      if (hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * multi_half(P), h->s) != hipSuccess)
         return bail(fail(GPK_EHIP, "initialise the panel slots"));
     }
     if (h->chain_aug) {

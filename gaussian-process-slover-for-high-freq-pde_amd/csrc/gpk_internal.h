@@ -203,9 +203,12 @@ struct ChainArgs {
   double* Od; int ldod;                    // K^{-1} D^T
   double* PBa; int ldpba;                  // augmented panel buffer [p][32*(tu+td)]
   double* gran;                            // pivot-chain input slots [T][2][1024], CHAIN_SENTINEL
-  double* PB2; unsigned int* epoch;        // chain_multi: panel slots [2][p*p] (CHAIN_SENTINEL),
-                                           // launch counter (zeroed)
+  double* PB2; unsigned int* epoch;        // chain_multi: hand-off slots [2][multi_half(p)]
+                                           // (CHAIN_SENTINEL), launch counter (zeroed)
 };
+// one launch-parity half of chain_multi's hand-off slots: the panel [p*p], then L_k^{-1} of every
+// pivot [p/32][1024]
+__host__ __device__ inline size_t multi_half(int p) { return (size_t)p * p + (size_t)32 * p; }
 // bit pattern of an unwritten hand-off word: a signalling NaN (quiet bit clear), which no
 // floating-point operation returns; equal 32-bit halves (hipMemsetD32 fills it)
 constexpr unsigned long long CHAIN_SENTINEL = 0x7ff4dead7ff4deadull;

@@ -281,7 +281,7 @@ __device__ __forceinline__ bool gran_ok(double v) {
 template <bool ONEWAVE>
 __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc, double* sXJ,
                                              double* sP, double* sM, double* pv, bool trm,
-                                             bool early_flag) {
+                                             bool early_flag, double* lw = nullptr) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int tx = t & 31, ty = t >> 5;
@@ -337,9 +337,11 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
       ls = pivot_chol_inv_1w<double*, PivotPrefetch>(sP, sM, pv, t, F.status, &s_pflag, hook);
     else
       ls = pivot_chol_inv_block<4, double*, PivotPrefetch>(sP, sM, pv, t, F.status, hook);
-    for (int e = t; e < 1024; e += 256) st_sc1(F.piv + (size_t)kp * 1024 + e, sM[(e >> 5) * SP + (e & 31)]);
+    // lw (chain_multi): L^{-1}_kp as self-validating words in this launch's slots, no flag
+    double* ldst = (lw ? lw : F.piv) + (size_t)kp * 1024;
+    for (int e = t; e < 1024; e += 256) st_sc1(ldst + e, sM[(e >> 5) * SP + (e & 31)]);
     if (t == 0) F.ldet[kp] = ls;
-    if (kp + 1 == T) signal_flag(piv_rdy + kp);
+    if (kp + 1 == T && !lw) signal_flag(piv_rdy + kp);
     if (trm && kp > 0 && kp < 17) TR_HI(SLOT_SWEEP_PIVOT + kp - 1);
     if (trm && kp == 0) TR_HI(SLOT_PIVOT0);
   };
@@ -352,12 +354,18 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
                        __HIP_MEMORY_SCOPE_AGENT);
   }
   if (t == 0) s_pflag = 0;  // (the barrier inside factor(0) orders it before the pivot)
+  // lw: no pivot flags -- the zeroing above completes before any L^{-1} word is stored (every
+  // diagonal tile's atomicMax comes after it has read L^{-1}_0's words)
+  if (lw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   factor(0);  // acc = tile (0, 0) of K, gathered above
   for (int k = 0; k + 1 < T; ++k) {
     // L_k's flag: raised inside the hop (below); with early_flag (chain_multi, whose inputs are
     // usually late) at once -- its stores drain while the inputs are awaited, and the tile
     // workgroups' sweep k (which produces pivot k+2's inputs) does not wait for this hop
-    if (early_flag) signal_flag(piv_rdy + k);
+    if (early_flag) {
+      if (lw) __syncthreads();
+      else signal_flag(piv_rdy + k);
+    }
     bool ok = true;
 #pragma unroll
     for (int r = 0; r < 4; ++r) ok = ok && gran_ok(gx[r]) && gran_ok(gd[r]);
@@ -697,14 +705,17 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
   const int tx = t & 31, ty = t >> 5;
-  unsigned int* piv_rdy = F.flags + T * T;
   unsigned int* done = F.flags + T * T + 2 * T;
   // panel hand-off: self-validating words (chain_master's inputs, above) in the PB2 half of this
   // launch's parity; the other half (last launch's) is reset to the sentinel meanwhile, a chunk
   // per tile workgroup and sweep, off the critical path.  No flags, no drains.
+  // L_k^{-1} travels the same way (PLc, after the panel slots in each half; no pivot flags): it
+  // is normally written before the panel row it goes with, so it arrives with the panel's loads
   const unsigned ep = __hip_atomic_load(F.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  double* PBc = F.PB2 + (size_t)(ep & 1u) * p * p;
-  double* PBo = F.PB2 + (size_t)((ep & 1u) ^ 1u) * p * p;
+  const size_t hs = multi_half(p);
+  double* PBc = F.PB2 + (size_t)(ep & 1u) * hs;
+  double* PBo = F.PB2 + (size_t)((ep & 1u) ^ 1u) * hs;
+  double* PLc = PBc + (size_t)p * p;
   // LDS: L_k^{-1} [32][SA] + four swizzled V tiles; the pivot chain's sXJ / sP / sM alias them
   __shared__ double pool[32 * SA + 4 * 1024];
   __shared__ double pv[32];
@@ -767,7 +778,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
     double* sXJ = pool;             // [32][SB]
     double* sP = pool + 32 * SB;    // [32][SP]
     double* sM = sP + 32 * SP;      // [32][SP]
-    chain_master<false>(F, T, a0, sXJ, sP, sM, pv, trm, true);
+    chain_master<false>(F, T, a0, sXJ, sP, sM, pv, trm, true, PLc);
   }
 
   // hand-offs after sweep kk - 1 (kk = k + 1; kk = 0: before sweep 0): panel row kk -- tile
@@ -836,7 +847,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
   };
   if (!master) publish_stores(0);
   // this workgroup's share of the other half's reset: [rs0, rs1), a chunk per sweep
-  const size_t ntot = (size_t)p * p;
+  const size_t ntot = hs;
   const int gidx = (int)blockIdx.x - ((int)blockIdx.x > mpos ? 1 : 0);
   const size_t share = (ntot + (nwg - 2)) / (nwg - 1);
   const size_t rs0 = std::min(ntot, (size_t)gidx * share), rs1 = std::min(ntot, rs0 + share);
@@ -876,6 +887,23 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
         for (int r = 0; r < 4; ++r) ok = ok && gran_ok(xv[v][r]);
       return ok;
     };
+    // L_k^{-1}'s words (row ty + 8r, column tx), loaded with the panel's; only the words still
+    // holding the sentinel are loaded again
+    const double* Li = PLc + (size_t)k * 1024;
+    double lv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lv[r] = __longlong_as_double((long long)CHAIN_SENTINEL);
+    auto load_l = [&]() {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!gran_ok(lv[r])) lv[r] = ld_sc1(Li + (ty + 8 * r) * 32 + tx);
+    };
+    auto l_ok = [&]() {
+      bool ok = true;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ok = ok && gran_ok(lv[r]);
+      return ok;
+    };
     load_panel();
     for (unsigned spins = 0; !panel_ok(); ++spins) {
       if (spins == (1u << 22)) {
@@ -886,14 +914,23 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
       load_panel();
     }
     if (trc) TR_HI(SLOT_MC_PANEL + k);
-    if (t == 0) wait_flag(piv_rdy + k, F.status);
+    // L_k^{-1} only once the panel is in: polling both together had ~500 workgroups re-loading
+    // the same 8 KB while the pivot was being factored (measured: C2 0.638 -> 0.676 ms)
+    load_l();
+    for (unsigned spins = 0; !l_ok(); ++spins) {
+      if (spins == (1u << 22)) {
+        atomicOr(F.status, 2);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      load_l();
+    }
     if (trc) TR_HI(SLOT_MC_PIV + k);
     __syncthreads();
-    const double* Li = F.piv + (size_t)k * 1024;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = ty + 8 * r;
-      sL[row * SA + tx] = ld_sc1(Li + row * 32 + tx);
+      sL[row * SA + tx] = lv[r];
 #pragma unroll
       for (int v = 0; v < 4; ++v)
         if (need[v]) sV[v * 1024 + vsw(row, tx)] = xv[v][r];

@@ -34,7 +34,7 @@ for k in range(16):
     NAMES[67 + 4 * k] = f"  gemm {k} last wg"
 for k in range(16):
     NAMES[128 + k] = f"mc sweep {k}: panel loads issued"
-    NAMES[144 + k] = f"mc sweep {k}: L flag seen"
+    NAMES[144 + k] = f"mc sweep {k}: L words in"
     NAMES[160 + k] = f"mc sweep {k}: L + panel in LDS"
     NAMES[176 + k] = f"mc sweep {k}: V in LDS"
     NAMES[192 + k] = f"mc sweep {k}: pass-0 published"
