@@ -887,6 +887,22 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
         for (int r = 0; r < 4; ++r) ok = ok && gran_ok(xv[v][r]);
       return ok;
     };
+    // re-load while waiting: only each tile's first word (r = 0) until those are in, then the
+    // words still holding the sentinel -- a quarter of the polling traffic of ~500 waiting
+    // workgroups, which otherwise delays the very stores they wait for
+    auto reload_panel = [&]() {
+      bool head = true;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) head = head && gran_ok(xv[v][0]);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int idx = v < 2 ? 2 * R + v : 2 * c0 + (v - 2);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (need[v] && !gran_ok(xv[v][r]) && (r == 0 || head))
+            xv[v][r] = ld_sc1(PBc + (size_t)(k * 32 + ty + 8 * r) * p + idx * 32 + tx);
+      }
+    };
     // L_k^{-1}'s words (row ty + 8r, column tx), loaded with the panel's; only the words still
     // holding the sentinel are loaded again
     const double* Li = PLc + (size_t)k * 1024;
@@ -911,7 +927,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
         break;
       }
       __builtin_amdgcn_s_sleep(1);
-      load_panel();
+      reload_panel();
     }
     if (trc) TR_HI(SLOT_MC_PANEL + k);
     // L_k^{-1} only once the panel is in: polling both together had ~500 workgroups re-loading
