@@ -152,6 +152,10 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
   const ClassArgs& C = A.cls;
   const int n = A.n, p = A.p;
   if (band * 64 >= n || chunk >= C.nchunk) return;  // shorter axis
+  // 1D (lower pairs only): a chunk whose rows all lie above the band's diagonals has no pair; its
+  // partials stay the zeros they were allocated with (nobody else writes them), so the ~half of
+  // the grid above the diagonal ends here instead of zeroing LDS bins and storing zeros
+  if (MODE1D && min(n, chunk * C.rb + C.rb) - 1 < band * 64) return;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   if (TR_FIRST) TR_LO(SLOT_CLASS_SUM);
   if (TR_LAST) TR_LO(SLOT_CSUM_START);

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r3lw
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_chain_multi.py -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/r3lw/pytest.log 2>&1 || { tail -30 gpurun_out/r3lw/pytest.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gpu_chain_multi.py tests/test_gpu_parity.py tests/test_gpu_golden.py -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/r3lw/pytest.log 2>&1 || { tail -30 gpurun_out/r3lw/pytest.log; exit 1; }
 tail -1 gpurun_out/r3lw/pytest.log
 L=$PWD/gaussian-process-slover-for-high-freq-pde_amd/gpk/_lib
 GPK_LIB_PATH=$L/libgpk_trace.so timeout -k 10 200 python tools/timeline.py --config C2 --steps 5 > gpurun_out/r3lw/c2.txt 2>&1 || exit 1
