@@ -74,6 +74,15 @@ __device__ __forceinline__ double ld_wt(const double* p) {  // global_load sc1 (
 // sum_{k<n} p[k*stride] in index order (sc1 loads), 16 in flight per batch (latency-bound chain)
 __device__ __forceinline__ double strided_sum(const double* p, int stride, int n) {
   double acc = 0.0;
+  if (n > 16 && n <= 32) {  // (C2's levels: 25-26 partials) every load in flight at once, same order
+    double v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = ld_wt(p + (size_t)(j < n ? j : 0) * stride);
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if (j < n) acc += v[j];
+    return acc;
+  }
   int k = 0;
   for (; k + 16 <= n; k += 16) {
     double v[16];
