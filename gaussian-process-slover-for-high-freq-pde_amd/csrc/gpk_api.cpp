@@ -1483,7 +1483,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     // every hand-off slot starts unwritten (spdinv.hip chain_master / chain_multi_kernel)
     if (hipMemsetD32Async(h->cgran[a], CHAIN_SENTINEL32, (size_t)(P / 32) * 4096, h->s) != hipSuccess)
       return bail(fail(GPK_EHIP, "initialise the pivot-chain input slots"));
-    if (h->chain_multi) {
+    if (h->chain) {  // chain_multi: panel + L^{-1} slots; chain_kernel: the L^{-1} slots
       A_(h->PB2[a], 2 * multi_half(P));
       A_(h->cepoch[a], 4);
       if (hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * multi_half(P), h->s) != hipSuccess)

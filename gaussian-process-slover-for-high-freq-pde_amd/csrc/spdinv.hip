@@ -398,7 +398,7 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
     vj = mma_t(sM, SP, 1, sXJ, SB, 1, wr, wc, lane, vj);  // V = L_k^{-1} X_{k,k+1}
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // L^{-1}_k's stores (long drained)
     __syncthreads();
-    if (t == 0 && !early_flag) __hip_atomic_store(piv_rdy + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0 && !early_flag && !lw) __hip_atomic_store(piv_rdy + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     store_quad(sXJ, SB, wr, wc, lane, vj);
     __syncthreads();
     d4 prod = {0.0, 0.0, 0.0, 0.0};
@@ -442,6 +442,12 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
   __shared__ double sXI[32 * SB], sXJ[32 * SB];
   __shared__ double sP[32 * SP], sM[32 * SP], pv[32];
   __shared__ unsigned int s_last;
+  // L_k^{-1} as self-validating words (chain_multi_kernel's form) in this launch's half of the
+  // L^{-1} slots (PB2, launch parity; the other half is reset by the last workgroup): the tile
+  // workgroups see L_k^{-1} as soon as its stores land instead of after the pivot chain's flag,
+  // which it raises only inside the next hop
+  const unsigned ep = F.PB2 ? __hip_atomic_load(F.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  double* PLc = F.PB2 ? F.PB2 + (size_t)(ep & 1u) * multi_half(p) + (size_t)p * p : nullptr;
 
   // own tile, this wave's quadrant: rows 16 wr + (lane >> 4) + 4 r, column 16 wc + (lane & 15)
   d4 acc;
@@ -504,7 +510,7 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
   };
   const bool trm = t == 0 && m == 0;  // probes (gpk_trace.h): factor 0's pivot owners
   if (master) {
-    chain_master<true>(F, T, acc, sXJ, sP, sM, pv, trm, false);
+    chain_master<true>(F, T, acc, sXJ, sP, sM, pv, trm, false, PLc);
   } else {
     if (trm && tile == 0) TR_LO(SLOT_GATHER);
     chain_inputs(0);                       // tiles (0, 1) and (1, 1) as they are before sweep 0
@@ -531,15 +537,51 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
       xi[r] = needI ? ld_sc1(F.PB + (size_t)(k * 32 + row) * p + I * 32 + tx) : 0.0;
       xj[r] = needJ ? ld_sc1(panel_ptr(k, row, tx)) : 0.0;
     }
-    if (t == 0) wait_flag(piv_rdy + k, F.status);
-    __syncthreads();
     const bool trl = t == 0 && m == 0 && k == T - 1 && I == T - 1 && J == T - 1;
-    if (trl) TR_HI(SLOT_LAST_FLAG);
-    const double* Li = F.piv + (size_t)k * 1024;
+    double lv[4];
+    if (PLc) {
+      // one thread polls one word of L_k^{-1} (the polling traffic of a flag), then every thread
+      // loads its words and re-loads those still holding the sentinel (bounded)
+      const double* Lw = PLc + (size_t)k * 1024;
+      if (t == 0) {
+        for (unsigned spins = 0; !gran_ok(ld_sc1(Lw + 1023)); ++spins) {
+          if (spins == (1u << 22)) {
+            atomicOr(F.status, 2);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (trl) TR_HI(SLOT_LAST_FLAG);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lv[r] = ld_sc1(Lw + (ty + 8 * r) * 32 + tx);
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ok = ok && gran_ok(lv[r]);
+        if (ok) break;
+        if (spins == (1u << 22)) {
+          atomicOr(F.status, 2);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (!gran_ok(lv[r])) lv[r] = ld_sc1(Lw + (ty + 8 * r) * 32 + tx);
+      }
+    } else {
+      if (t == 0) wait_flag(piv_rdy + k, F.status);
+      __syncthreads();
+      if (trl) TR_HI(SLOT_LAST_FLAG);
+      const double* Li = F.piv + (size_t)k * 1024;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lv[r] = ld_sc1(Li + (ty + 8 * r) * 32 + tx);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = ty + 8 * r;
-      sL[row * SA + tx] = ld_sc1(Li + row * 32 + tx);
+      sL[row * SA + tx] = lv[r];
       if (needI) sXI[row * SB + tx] = xi[r];
       if (needJ) sXJ[row * SB + tx] = xj[r];
     }
@@ -611,6 +653,11 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
     for (int e = t; e < T * TC + 2 * T; e += 256)
       __hip_atomic_store(F.flags + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (PLc) {  // the other half's L^{-1} slots (last launch's) back to the sentinel; next parity
+      double* PLo = F.PB2 + (size_t)((ep & 1u) ^ 1u) * multi_half(p) + (size_t)p * p;
+      for (int e = t; e < T * 1024; e += 256) PLo[e] = __longlong_as_double((long long)CHAIN_SENTINEL);
+      if (t == 0) __hip_atomic_store(F.epoch, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -1112,7 +1159,8 @@ hipError_t launch_spd_chain(const ChainArgs* a, int nmat, int deriv, hipStream_t
     f.Ou = a[m].Ou; f.ldou = a[m].ldou; f.ou_t = a[m].ou_t; f.Od = a[m].Od; f.ldod = a[m].ldod;
     f.PBa = a[m].PBa; f.ldpba = a[m].ldpba;
     f.gran = a[m].gran; f.piv_off = f.T * (f.T + f.tu + f.td);
-    if ((a[m].cid != nullptr) != gather || !f.gran) return hipErrorInvalidValue;
+    f.PB2 = a[m].PB2; f.epoch = a[m].epoch;  // (both null: L^{-1} hand-off by flag + load)
+    if ((a[m].cid != nullptr) != gather || !f.gran || !f.PB2 != !f.epoch) return hipErrorInvalidValue;
     Tmax = std::max(Tmax, f.T * (f.T + f.tu + f.td) + 1);  // + the pivot chain's workgroup
   }
   dim3 grid(Tmax, nmat + (prep ? 1 : 0));
