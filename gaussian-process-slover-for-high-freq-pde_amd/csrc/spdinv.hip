@@ -515,6 +515,12 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
     if (trm && tile == 0) TR_LO(SLOT_GATHER);
     chain_inputs(0);                       // tiles (0, 1) and (1, 1) as they are before sweep 0
     if (I == 0 && J != 0) publish_tile();  // row 0 is the panel of sweep 0
+    if (PLc) {  // this tile's share of the other half's L^{-1} slots (last launch's) -> sentinel
+      double* PLo = F.PB2 + (size_t)((ep & 1u) ^ 1u) * multi_half(p) + (size_t)p * p;
+      const int share = (T * 1024 + T * TC - 1) / (T * TC);
+      const int e1 = min(T * 1024, (tile + 1) * share);
+      for (int e = tile * share + t; e < e1; e += 256) PLo[e] = __longlong_as_double((long long)CHAIN_SENTINEL);
+    }
   }
 
   for (int k = 0; k < T && !master; ++k) {
@@ -653,11 +659,7 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
     for (int e = t; e < T * TC + 2 * T; e += 256)
       __hip_atomic_store(F.flags + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (PLc) {  // the other half's L^{-1} slots (last launch's) back to the sentinel; next parity
-      double* PLo = F.PB2 + (size_t)((ep & 1u) ^ 1u) * multi_half(p) + (size_t)p * p;
-      for (int e = t; e < T * 1024; e += 256) PLo[e] = __longlong_as_double((long long)CHAIN_SENTINEL);
-      if (t == 0) __hip_atomic_store(F.epoch, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (PLc && t == 0) __hip_atomic_store(F.epoch, ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
