@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
   __shared__ double sP[32 * SP], sM[32 * SP], pv[32];
   __shared__ unsigned int s_last;
   // L_k^{-1} as self-validating words (chain_multi_kernel's form) in this launch's half of the
-  // L^{-1} slots (PB2, launch parity; the other half is reset by the last workgroup): the tile
+  // L^{-1} slots (PB2, launch parity; the other half is reset by the tile workgroups): the tile
   // workgroups see L_k^{-1} as soon as its stores land instead of after the pivot chain's flag,
   // which it raises only inside the next hop
   const unsigned ep = F.PB2 ? __hip_atomic_load(F.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
