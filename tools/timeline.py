@@ -23,7 +23,7 @@ NAMES = {0: "class_eval first wg", 1: "gather pivot wg | chain wg(0,0)", 2: "piv
          47: "pg last grad wg", 48: "pg first wg staged", 49: "class_sum last wg",
          50: "class_eval last wg", 51: "gather last wg", 52: "class_sum wg0 loaded", 53: "chain: last wg done",
          54: "chain: factor-1 pivot chain done", 55: "fin: loads issued", 56: "fin: sums done",
-         57: "fin: loss done", 58: "chain last sweep: L flag seen", 59: "chain last sweep: L in LDS",
+         57: "fin: loss done", 58: "chain last sweep: L word seen", 59: "chain last sweep: L in LDS",
          60: "chain last sweep: products done", 61: "chain last sweep: tile out + done",
          62: "chain last sweep: aug tile out + done", 36: "chain: prefetch missed (first..last)",
          37: "pg group complete (first..last)", 38: "pg U plane last wg"}
