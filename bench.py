@@ -77,8 +77,8 @@ def cpu_baseline(config, seconds, threads, max_steps=400, min_steps=1, warmup=Tr
     except Exception:  # pragma: no cover
         pass
     from oracle import gp_oracle as O
-    from gpk.problems import CONFIGS
-    cfg = CONFIGS[config]
+    from gpk.problems import get_config
+    cfg = get_config(config)
     n = cfg["n"]
     if cfg["dim"] == 1:
         prob, _, _ = O.setup_1d(cfg["equation"], n, cfg["scale"], cfg["kernel"],
@@ -178,7 +178,8 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
     broadcast over RCCL (GPK_FLAG_SPLIT_FACTORS) instead of both factors on every rank."""
     from gpk import replicas, shard
     from gpk._lib import GPK_FLAG_SPLIT_FACTORS
-    out = {}
+    from gpk.problems import make_solver
+    out, single = {}, {}
     for key in configs:
         cid = key.split("_")[0]
         flags = GPK_FLAG_SPLIT_FACTORS if key.endswith("_split") else 0
@@ -202,6 +203,11 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
         dt = replicas.max_over_ranks(t1 - t0, ctx)
         out[key] = {"value": steps / dt, "unit": "iters/s", "ms_per_step": dt / steps * 1e3,
                     "steps": steps, "ranks": ctx.world}
+        if cid not in single:
+            STAGE["name"] = f"sharded {key}: single-GPU reference on rank 0"
+            single[cid] = single_gpu_reference(lambda: make_solver(cid, seed=0), steps, ctx)
+        out[key].update(single[cid])
+        out[key]["speedup_vs_1gpu"] = single[cid]["single_gpu_ms_per_step"] / out[key]["ms_per_step"]
     # C5 is reported both ways: both factors inverted on every rank, or one factor
     # per rank half + a broadcast of K^{-1}; the default is the replicated form
     out["C5_default"] = "C5 (replicated inverse); C5_split = GPK_FLAG_SPLIT_FACTORS"
@@ -209,6 +215,28 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
 
 
 STAGE = {"name": "start"}   # what the sharded section is doing (reported when it fails)
+
+
+def single_gpu_reference(make, steps, ctx):
+    """The same problem unsharded on ONE GPU (rank 0, its own device; the other ranks wait at the
+    barrier): ms per step of `steps` timed steps after a prepared warm-up, the denominator of a
+    sharded entry's speedup_vs_1gpu (strong scaling, measured in the same run)."""
+    from gpk import replicas
+    ms = None
+    if ctx.rank == 0:
+        s = make()
+        try:
+            s.prepare(steps)
+            s.step(2)
+            s.sync()
+            t0 = time.perf_counter()
+            s.step(steps)
+            s.sync()
+            ms = (time.perf_counter() - t0) / steps * 1e3
+        finally:
+            s.close()
+    replicas.barrier(ctx)
+    return {"single_gpu_ms_per_step": ms, "single_gpu_steps": steps}
 
 
 def dry_run_sharded_section(a, ctx):
@@ -223,7 +251,11 @@ def dry_run_sharded_section(a, ctx):
         raise RuntimeError("stand-in collective failed")
     replicas.barrier(ctx)
     dt = replicas.max_over_ranks(1e-3, ctx)
-    return {"dry-run": {"value": 1.0 / dt, "unit": "iters/s", "ranks": ctx.world}}
+    out = {"value": 1.0 / dt, "unit": "iters/s", "ms_per_step": dt * 1e3, "ranks": ctx.world}
+    out.update(single_gpu_reference(lambda: _DryRunSolver(0), 3, ctx))
+    out["speedup_vs_1gpu"] = (out["single_gpu_ms_per_step"] / out["ms_per_step"]
+                              if out["single_gpu_ms_per_step"] is not None else None)
+    return {"dry-run": out}
 
 
 def kernel_roofline(s, cfg, iters):

@@ -22,6 +22,8 @@
 
 namespace gpk {
 
+GPK_WAIT_LIMIT_SETTER(wait_limit_assemble)  // gpk_set_wait_limit
+
 GPK_TRACE_TU(assemble)
 
 // Partial sums over components c = c0, c0 + cs, ... (cs = stride) of K and D at one pair.

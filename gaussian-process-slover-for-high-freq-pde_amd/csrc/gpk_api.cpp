@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <sched.h>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -1093,11 +1094,10 @@ static int capture_call(gpk_handle* h, bool fast) {
   const size_t np = (size_t)h->L.nparams;
   hipGraph_t g = nullptr;
   HIPCHK(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
-  StepBegin b{};
-  if (fast) {
-    b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
-    b.snap_count = h->snap_count; b.count = h->count; b.viol = h->viol;
-  }
+  StepBegin b{};  // every batch takes the snapshot: a failed one is undone (read_report)
+  b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
+  b.snap_count = h->snap_count; b.count = h->count;
+  if (fast) b.viol = h->viol;
   b.loss_slot = h->loss_slot;
   const StepReport r = make_report(h, fast, 1);
   int rc = begin_batch(h, &b);
@@ -1166,7 +1166,7 @@ static int reset_handoffs(gpk_handle* h) {
     const size_t P = a == 0 ? L.p1 : L.p2, T = P / 32;
     const size_t nflags = T * (T + (L.p1 + L.p2) / 32) + 2 * T + 1;
     HIPCHK(hipMemsetD32Async(h->cgran[a], CHAIN_SENTINEL32, T * 4096, h->s));
-    if (h->PB2[a]) HIPCHK(hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * multi_half((int)P), h->s));
+    if (h->PB2[a]) HIPCHK(hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * chain_half((int)P, h->chain_multi), h->s));
     if (h->cepoch[a]) HIPCHK(hipMemsetAsync(h->cepoch[a], 0, 4 * sizeof(unsigned int), h->s));
     HIPCHK(hipMemsetAsync(h->cflags[a], 0, nflags * sizeof(unsigned int), h->s));
     HIPCHK(hipMemsetAsync(h->aflag[a], 0, 4 * sizeof(unsigned int), h->s));
@@ -1198,6 +1198,18 @@ static int read_status(gpk_handle* h) {
 constexpr double FAST_GRAPH_MARGIN = 8.0;
 static int read_report(gpk_handle* h, bool fast, bool* violated);
 
+// params, Adam state and step count back to the snapshot the current batch's begin took (every
+// gpk_step batch takes one), U's padded copy rebuilt from params: a fast batch that met an open
+// refinement gate is rerun from there, a batch that failed on the device is undone
+static int restore_snapshot(gpk_handle* h) {
+  const size_t np = (size_t)h->L.nparams, nb = np * sizeof(double);
+  HIPCHK(hipMemcpyAsync(h->params, h->snap, nb, hipMemcpyDeviceToDevice, h->s));
+  HIPCHK(hipMemcpyAsync(h->m, h->snap + np, nb, hipMemcpyDeviceToDevice, h->s));
+  HIPCHK(hipMemcpyAsync(h->v, h->snap + 2 * np, nb, hipMemcpyDeviceToDevice, h->s));
+  HIPCHK(hipMemcpyAsync(h->count, h->snap_count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
+  return check_launch(launch_sync_u(h->params, h->L, h->Up, h->s), "sync_u");
+}
+
 static int finish_batch(gpk_handle* h, bool fast, bool* violated) {
   TRY(check_launch(launch_step_report(make_report(h, fast, h->pend_losses ? h->pend_n : 0), h->s),
                    "step_report"));
@@ -1214,11 +1226,15 @@ static int read_report(gpk_handle* h, bool fast, bool* violated) {
   const unsigned int vi = (unsigned int)h->rep_host[1];
   double ps[2][2] = {{h->rep_host[2], h->rep_host[3]}, {h->rep_host[4], h->rep_host[5]}};
   *violated = false;
-  if (st) {
+  if (st) {  // undo the batch (its begin took the snapshot), then report
     HIPCHK(hipMemsetAsync(h->status, 0, sizeof(int), h->s));
     if (st & 2) TRY(reset_handoffs(h));
-    return fail(GPK_ENOTPD, (st & 2) ? "SPD inverse: a pivot-chain hand-off timed out (device status 2)"
-                                      : "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
+    TRY(restore_snapshot(h));
+    HIPCHK(hipStreamSynchronize(h->s));
+    return fail(GPK_ENOTPD, (st & 2) ? "SPD inverse: a pivot-chain hand-off timed out (device status 2); "
+                                       "the batch was undone"
+                                     : "covariance factor is not positive definite (non-positive pivot in SPD inverse); "
+                                       "the batch was undone");
   }
   *violated = fast && vi;
   if (h->fast_ok) {
@@ -1417,8 +1433,12 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     const bool in_group = shard && local_group && nranks > 1;
     if (shard && nranks >= 2 && (p->flags & GPK_FLAG_SPLIT_FACTORS)) h->split_axis = rank < nranks / 2 ? 0 : 1;
     // (the chain inverts every factor in one launch: a split rank inverts one, per sweep)
-    h->chain = !h->bigspd && !in_group && h->split_axis < 0 && !(p->flags & GPK_FLAG_NO_CHAIN) &&
-               grid_blocks(false) <= cap;
+    // (an in-process group's ranks launch their chains concurrently on the one device: all of
+    // them must be co-resident together -- the 2-rank group is how the tests exercise the exact
+    // chain + row-sharded step an RCCL rank runs)
+    const int chains_on_device = in_group ? nranks : 1;
+    h->chain = !h->bigspd && h->split_axis < 0 && !(p->flags & GPK_FLAG_NO_CHAIN) &&
+               grid_blocks(false) * chains_on_device <= cap;
     h->chain_aug = h->chain && L.dim == 2 && !shard && !(p->flags & GPK_FLAG_NO_CHAIN_AUG) &&
                    grid_blocks(true) <= cap;
     // large 1D factors: the persistent inverse on 64-row macro tiles (chain_multi_kernel), when
@@ -1484,9 +1504,9 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     if (hipMemsetD32Async(h->cgran[a], CHAIN_SENTINEL32, (size_t)(P / 32) * 4096, h->s) != hipSuccess)
       return bail(fail(GPK_EHIP, "initialise the pivot-chain input slots"));
     if (h->chain) {  // chain_multi: panel + L^{-1} slots; chain_kernel: the L^{-1} slots
-      A_(h->PB2[a], 2 * multi_half(P));
+      A_(h->PB2[a], 2 * chain_half(P, h->chain_multi));
       A_(h->cepoch[a], 4);
-      if (hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * multi_half(P), h->s) != hipSuccess)
+      if (hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * chain_half(P, h->chain_multi), h->s) != hipSuccess)
         return bail(fail(GPK_EHIP, "initialise the panel slots"));
     }
     if (h->chain_aug) {
@@ -1679,24 +1699,36 @@ static int group_run(gpk_handle** hs, int nranks, int apply, int n_steps) {
   for (auto& t : th) t.join();
   for (int r = 0; r < nranks; ++r)
     if (rcs[r] != GPK_OK) return fail(rcs[r], "rank " + std::to_string(r) + ": " + errs[r]);
-  // every rank's status: a group whose ranks disagree (some report a non-PD factor, some not)
-  // would, under RCCL, leave the reporting ranks out of the next step's collectives -- the step
-  // makes the status group-wide (split_broadcast); a disagreement here is an internal error
-  int rc = GPK_OK, bad = 0;
-  std::string first;
+  // every rank's status: a group whose ranks disagree about a non-PD factor would, under RCCL,
+  // leave the reporting ranks out of the next step's collectives -- the step makes that status
+  // group-wide (split_broadcast), so such a disagreement is an internal error.  A hand-off
+  // timeout (bit 2) is rank-local by nature (a wait of one rank's launch gave up): it fails the
+  // whole group with GPK_ENOTPD, and every rank's hand-off slots are reset.
+  std::vector<int> st(nranks, 0);
+  int any = 0, bad = 0;
   for (int r = 0; r < nranks; ++r) {
     DevSwitch ds(hs[r]->dev);
-    const int rr = read_status(hs[r]);
-    if (rr != GPK_OK) {
-      if (!bad++) first = g_err;
-      rc = rr;
-    }
+    HIPCHK(hipMemcpy(&st[r], hs[r]->status, sizeof(int), hipMemcpyDeviceToHost));
+    any |= st[r];
+    bad += st[r] != 0;
   }
-  if (bad && bad != nranks)
+  if (!any) return GPK_OK;
+  for (int r = 0; r < nranks; ++r) {
+    DevSwitch ds(hs[r]->dev);
+    HIPCHK(hipMemsetAsync(hs[r]->status, 0, sizeof(int), hs[r]->s));
+    if (any & 2) TRY(reset_handoffs(hs[r]));
+    HIPCHK(hipStreamSynchronize(hs[r]->s));
+  }
+  if (any & 2) {
+    int r0 = 0;
+    while (!(st[r0] & 2)) ++r0;
+    return fail(GPK_ENOTPD, "SPD inverse: a pivot-chain hand-off timed out (device status 2, rank " +
+                                std::to_string(r0) + ")");
+  }
+  if (bad != nranks)
     return fail(GPK_EINVAL, "internal: device status differs across the ranks of the group (" +
-                                std::to_string(bad) + " of " + std::to_string(nranks) + "): " + first);
-  if (rc != GPK_OK) return fail(rc, first);
-  return GPK_OK;
+                                std::to_string(bad) + " of " + std::to_string(nranks) + ")");
+  return fail(GPK_ENOTPD, "covariance factor is not positive definite (non-positive pivot in SPD inverse)");
 }
 
 int gpk_group_step(gpk_handle** hs, int32_t nranks, int32_t n_steps, double* losses) {
@@ -1902,6 +1934,11 @@ static int wait_report(gpk_handle* h) {
   volatile double* ready = reinterpret_cast<volatile double*>(h->rep_host) + 7;
   for (unsigned it = 1;; ++it) {
     if (*ready != 0.0) break;
+    // back-off: tight for the first 2^14 reads (a C4 step's report lands within ~100 us), then
+    // a pause per read, then a yield per read past 2^20 (a C5 call waits tens of ms: the host
+    // core is left to others instead of spinning flat out)
+    if (it > (1u << 20)) sched_yield();
+    else if (it > (1u << 14)) __builtin_ia32_pause();
     if ((it & 4095u) == 0) {
       const hipError_t e = hipStreamQuery(h->s);
       if (e == hipErrorNotReady) continue;
@@ -1926,7 +1963,7 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
   if (n_steps < 0) return fail(GPK_EINVAL, "n_steps < 0");
   DevSwitch ds(h->dev);
   h->pend_losses = nullptr;  // (a failed earlier call may have left one)
-  const size_t np = (size_t)h->L.nparams, nb = np * sizeof(double);
+  const size_t np = (size_t)h->L.nparams;
   int done = 0;
   if (n_steps == 1 && !h->shard) {  // one graph launch per call (a rollback takes the path below)
     const bool fast = h->fast_ok && h->fast_mode;
@@ -1939,11 +1976,7 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
     TRY(read_report(h, fast, &viol));
     if (!viol) return GPK_OK;
     ++h->rollbacks;  // restore the snapshot the call graph took and rerun with the full graph
-    HIPCHK(hipMemcpyAsync(h->params, h->snap, nb, hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemcpyAsync(h->m, h->snap + np, nb, hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemcpyAsync(h->v, h->snap + 2 * np, nb, hipMemcpyDeviceToDevice, h->s));
-    HIPCHK(hipMemcpyAsync(h->count, h->snap_count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
-    TRY(check_launch(launch_sync_u(h->params, h->L, h->Up, h->s), "sync_u"));
+    TRY(restore_snapshot(h));
     TRY(capture_call(h, false));
     arm_report(h);
     HIPCHK(hipGraphLaunch(h->g_call[1], h->s));
@@ -1969,10 +2002,9 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
       {  // the snapshot of everything a fast batch carries forward (Up is rebuilt from params),
          // the violation flag and the loss slot: one launch
         StepBegin b{};
-        if (fast) {
-          b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
-          b.snap_count = h->snap_count; b.count = h->count; b.viol = h->viol;
-        }
+        b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = np;
+        b.snap_count = h->snap_count; b.count = h->count;
+        if (fast) b.viol = h->viol;
         b.loss_slot = h->loss_slot;
         TRY(check_launch(launch_step_begin(b, h->s), "step_begin"));
       }
@@ -1981,11 +2013,7 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
     }
     if (viol) {  // a step of the chunk needed refinement: roll back and rerun with the full graph
       ++h->rollbacks;
-      HIPCHK(hipMemcpyAsync(h->params, h->snap, nb, hipMemcpyDeviceToDevice, h->s));
-      HIPCHK(hipMemcpyAsync(h->m, h->snap + np, nb, hipMemcpyDeviceToDevice, h->s));
-      HIPCHK(hipMemcpyAsync(h->v, h->snap + 2 * np, nb, hipMemcpyDeviceToDevice, h->s));
-      HIPCHK(hipMemcpyAsync(h->count, h->snap_count, sizeof(int), hipMemcpyDeviceToDevice, h->s));
-      TRY(check_launch(launch_sync_u(h->params, h->L, h->Up, h->s), "sync_u"));
+      TRY(restore_snapshot(h));
       TRY(capture(h, 1, true));
       TRY(run_steps(h, n, lo, false));
       TRY(finish_batch(h, false, &viol));
@@ -2080,6 +2108,15 @@ int gpk_set_spd_big_workgroups(int32_t workgroups) {
 
 int gpk_set_chain_capacity(int32_t workgroups) {
   g_chain_cap.store(workgroups > 0 ? workgroups : 0);
+  return GPK_OK;
+}
+
+int gpk_set_wait_limit(int32_t polls) {
+  if (polls < 0) return fail(GPK_EINVAL, "polls must be >= 0");
+  const unsigned v = polls > 0 ? (unsigned)polls : SPIN_CAP;
+  if (wait_limit_spdinv(v) != hipSuccess || wait_limit_spdbig(v) != hipSuccess ||
+      wait_limit_assemble(v) != hipSuccess)
+    return fail(GPK_EHIP, "set the wait limit");
   return GPK_OK;
 }
 

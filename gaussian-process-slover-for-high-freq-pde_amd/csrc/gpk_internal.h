@@ -209,6 +209,9 @@ struct ChainArgs {
 // one launch-parity half of chain_multi's hand-off slots: the panel [p*p], then L_k^{-1} of every
 // pivot [p/32][1024]
 __host__ __device__ inline size_t multi_half(int p) { return (size_t)p * p + (size_t)32 * p; }
+// one launch-parity half of a chain handle's hand-off slots: chain_multi_kernel's panel slots +
+// L^{-1} slots (multi_half), chain_kernel's L^{-1} slots alone (T x 32 x 32 words)
+__host__ __device__ inline size_t chain_half(int p, bool multi) { return multi ? multi_half(p) : (size_t)32 * p; }
 // bit pattern of an unwritten hand-off word: a signalling NaN (quiet bit clear), which no
 // floating-point operation returns; equal 32-bit halves (hipMemsetD32 fills it)
 constexpr unsigned long long CHAIN_SENTINEL = 0x7ff4dead7ff4deadull;
@@ -264,6 +267,12 @@ size_t spd_big_piv_doubles(int p);
 // tile workgroups per factor of the update launch (0: two per CU); tests use a few to get long
 // runs of tiles per workgroup at small sizes
 void spd_big_set_workgroups(int g);
+// default poll budget of every bounded inter-workgroup wait (spd_pivot.h)
+constexpr unsigned SPIN_CAP = 1u << 22;
+// the bounded waits' poll budget of each translation unit that waits (spd_pivot.h g_wait_limit)
+hipError_t wait_limit_spdinv(unsigned polls);
+hipError_t wait_limit_spdbig(unsigned polls);
+hipError_t wait_limit_assemble(unsigned polls);
 hipError_t launch_spd_inverse_big(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
 // stage -1: pivot 0; 2k: panel of sweep k; 2k+1: update of sweep k
 hipError_t launch_spd_big_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);

@@ -13,16 +13,33 @@ typedef __attribute__((address_space(3))) double* lds_ptr;
 // bit 2 -- the step then reports GPK_ENOTPD ("hand-off timed out") instead of hanging the device
 // (a producer that is not resident, e.g. another process holding the CUs).  The host resets the
 // hand-off slots after such a launch (gpk_api.cpp reset_handoffs).
-constexpr unsigned SPIN_CAP = 1u << 22;
+// The poll budget, per translation unit that waits (spdinv, spdinv_big, assemble): SPIN_CAP
+// unless gpk_set_wait_limit lowered it (tests force a timeout with 1: every wait whose first
+// poll fails gives up).  A scalar constant-cache load per poll.
+static __constant__ unsigned g_wait_limit = SPIN_CAP;
+#define GPK_WAIT_LIMIT_SETTER(fn) \
+  hipError_t fn(unsigned polls) { return hipMemcpyToSymbol(HIP_SYMBOL(g_wait_limit), &polls, sizeof polls); }
+
+// Called on every poll of a wait that has not succeeded yet.  A wait gives up (status bit 2)
+// when its budget is spent, or -- read every 64th poll, so a hand-off that arrives within 63
+// polls (every one of a healthy step's critical hand-offs) costs no status load -- when another
+// wait of the same handle already gave up (bit 2 set): its producer may be gone, and the rest of
+// the grid and the later steps of a captured batch must drain within 64 polls per wait instead
+// of each spending the whole budget.
+__device__ __forceinline__ bool spin_give_up(unsigned spins, int* status) {
+  bool give_up = spins + 1 >= g_wait_limit;
+  if (!give_up && (spins & 63u) == 63u)
+    give_up = (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2) != 0;
+  if (give_up) atomicOr(status, 2);
+  return give_up;
+}
+
 template <int SLEEP = 1>
 __device__ __forceinline__ bool spin_until_ge(const unsigned int* c, unsigned int target, int* status) {
   for (unsigned spins = 0;
        __hip_atomic_load(const_cast<unsigned int*>(c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;
        ++spins) {
-    if (spins == SPIN_CAP) {
-      atomicOr(status, 2);
-      return false;
-    }
+    if (spin_give_up(spins, status)) return false;
     __builtin_amdgcn_s_sleep(SLEEP);
   }
   return true;

@@ -30,6 +30,8 @@
 
 namespace gpk {
 
+GPK_WAIT_LIMIT_SETTER(wait_limit_spdinv)  // gpk_set_wait_limit
+
 GPK_TRACE_TU(spdinv)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
@@ -374,10 +376,7 @@ __device__ __forceinline__ void chain_master(const ChainFactor& F, int T, d4 acc
     // hand-off that never arrives flags the status word (the step reports an error) instead of
     // hanging the device.
     for (unsigned spins = 0; !ok; ++spins) {
-      if (spins == (1u << 22)) {
-        atomicOr(F.status, 2);
-        break;
-      }
+      if (spin_give_up(spins, F.status)) break;
       __builtin_amdgcn_s_sleep(1);
       issue(k);
       ok = true;
@@ -447,7 +446,7 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
   // workgroups see L_k^{-1} as soon as its stores land instead of after the pivot chain's flag,
   // which it raises only inside the next hop
   const unsigned ep = F.PB2 ? __hip_atomic_load(F.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-  double* PLc = F.PB2 ? F.PB2 + (size_t)(ep & 1u) * multi_half(p) + (size_t)p * p : nullptr;
+  double* PLc = F.PB2 ? F.PB2 + (size_t)(ep & 1u) * chain_half(p, false) : nullptr;
 
   // own tile, this wave's quadrant: rows 16 wr + (lane >> 4) + 4 r, column 16 wc + (lane & 15)
   d4 acc;
@@ -516,7 +515,7 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
     chain_inputs(0);                       // tiles (0, 1) and (1, 1) as they are before sweep 0
     if (I == 0 && J != 0) publish_tile();  // row 0 is the panel of sweep 0
     if (PLc) {  // this tile's share of the other half's L^{-1} slots (last launch's) -> sentinel
-      double* PLo = F.PB2 + (size_t)((ep & 1u) ^ 1u) * multi_half(p) + (size_t)p * p;
+      double* PLo = F.PB2 + (size_t)((ep & 1u) ^ 1u) * chain_half(p, false);
       const int share = (T * 1024 + T * TC - 1) / (T * TC);
       const int e1 = min(T * 1024, (tile + 1) * share);
       for (int e = tile * share + t; e < e1; e += 256) PLo[e] = __longlong_as_double((long long)CHAIN_SENTINEL);
@@ -551,10 +550,7 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
       const double* Lw = PLc + (size_t)k * 1024;
       if (t == 0) {
         for (unsigned spins = 0; !gran_ok(ld_sc1(Lw + 1023)); ++spins) {
-          if (spins == (1u << 22)) {
-            atomicOr(F.status, 2);
-            break;
-          }
+          if (spin_give_up(spins, F.status)) break;
           __builtin_amdgcn_s_sleep(1);
         }
       }
@@ -567,10 +563,7 @@ __global__ __launch_bounds__(256, 2) void chain_kernel(ChainBatch b) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) ok = ok && gran_ok(lv[r]);
         if (ok) break;
-        if (spins == (1u << 22)) {
-          atomicOr(F.status, 2);
-          break;
-        }
+        if (spin_give_up(spins, F.status)) break;
         __builtin_amdgcn_s_sleep(1);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -971,10 +964,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
     };
     load_panel();
     for (unsigned spins = 0; !panel_ok(); ++spins) {
-      if (spins == (1u << 22)) {
-        atomicOr(F.status, 2);
-        break;
-      }
+      if (spin_give_up(spins, F.status)) break;
       __builtin_amdgcn_s_sleep(1);
       reload_panel();
     }
@@ -983,10 +973,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
     // the same 8 KB while the pivot was being factored (measured: C2 0.638 -> 0.676 ms)
     load_l();
     for (unsigned spins = 0; !l_ok(); ++spins) {
-      if (spins == (1u << 22)) {
-        atomicOr(F.status, 2);
-        break;
-      }
+      if (spin_give_up(spins, F.status)) break;
       __builtin_amdgcn_s_sleep(1);
       load_l();
     }

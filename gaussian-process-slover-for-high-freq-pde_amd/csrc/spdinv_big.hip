@@ -40,6 +40,8 @@
 
 namespace gpk {
 
+GPK_WAIT_LIMIT_SETTER(wait_limit_spdbig)  // gpk_set_wait_limit
+
 GPK_TRACE_TU(spdbig)
 
 static std::atomic<int> g_big_wgs{0};  // spd_big_set_workgroups override (tests)

@@ -177,20 +177,17 @@ hipError_t launch_step_begin(const StepBegin& b, hipStream_t s) {
 // batch's losses in one record written straight into pinned host memory (no device-to-host copies)
 __global__ void step_report_kernel(StepReport r) {
   for (int k = threadIdx.x; k < r.nloss; k += blockDim.x) r.out[8 + k] = r.losses[k];
-  if (threadIdx.x != 0) {
-    __threadfence_system();
-    __syncthreads();
-    return;
+  if (threadIdx.x == 0) {
+    r.out[0] = (double)*r.status;
+    r.out[1] = r.viol ? (double)*r.viol : 0.0;
+    for (int a = 0; a < 2; ++a) {
+      r.out[2 + 2 * a] = r.pst[a] ? r.pst[a][0] : 0.0;
+      r.out[3 + 2 * a] = r.pst[a] ? r.pst[a][1] : 0.0;  // (bits of max diag K^{-1})
+    }
   }
-  r.out[0] = (double)*r.status;
-  r.out[1] = r.viol ? (double)*r.viol : 0.0;
-  for (int a = 0; a < 2; ++a) {
-    r.out[2 + 2 * a] = r.pst[a] ? r.pst[a][0] : 0.0;
-    r.out[3 + 2 * a] = r.pst[a] ? r.pst[a][1] : 0.0;  // (bits of max diag K^{-1})
-  }
-  __threadfence_system();
+  __threadfence_system();  // every thread's record stores, then one barrier for the whole block
   __syncthreads();
-  report_ready(r.out);
+  if (threadIdx.x == 0) report_ready(r.out);
 }
 
 hipError_t launch_step_report(const StepReport& r, hipStream_t s) {

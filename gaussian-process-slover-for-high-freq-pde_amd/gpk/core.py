@@ -301,6 +301,12 @@ def set_spd_big_workgroups(workgroups):
     check(_lib.load().gpk_set_spd_big_workgroups(int(workgroups)))
 
 
+def set_wait_limit(polls):
+    """Poll budget of every inter-workgroup wait of later launches (0: the default 2^22).  Tests
+    use 1 to force the hand-off-timeout path (GPK_ENOTPD, the failed gpk_step batch undone)."""
+    check(_lib.load().gpk_set_wait_limit(int(polls)))
+
+
 def comm_unique_id():
     """128-byte RCCL id for gpk_create_sharded (rank 0 makes it, every rank uses the same)."""
     buf = (ctypes.c_uint8 * 128)()

@@ -23,6 +23,21 @@ CONFIGS = {
                scale=1.0, freq_scale=40.0, llk_weight=500.0, beta=200.0),
 }
 
+# The reference's own committed runs (code/result_log/*/kernel_Matern52_Cos_1d/epoch_100/Q30/
+# log.txt:2: N_col 400, Q 30, lr 0.01, freq_scale 20): the configs its run times -- the CPU
+# baseline's calibration points -- not BASELINE.json configs.
+REFERENCE_RUNS = {
+    "R1": dict(dim=1, equation="poisson_1d-single_sin", kernel="Matern52_Cos_1d", n=400,
+               scale=2 * np.pi, freq_scale=20.0, llk_weight=200.0),
+    "R2": dict(dim=2, equation="poisson_2d-sin_sin", kernel="Matern52_Cos_1d", n=400,
+               scale=2 * np.pi, freq_scale=20.0, llk_weight=200.0),
+}
+
+
+def get_config(name):
+    """A BASELINE config (C1..C5) or a reference run (R1, R2) by name."""
+    return CONFIGS[name] if name in CONFIGS else REFERENCE_RUNS[name]
+
 
 def problem_arrays(cfg):
     """Host arrays (x1, x2, src, bvals, bidx) for a config dict."""
@@ -41,7 +56,7 @@ def problem_arrays(cfg):
 def make_solver(config, seed=0, device=0, Q=30, lr=0.01, random_u=True, flags=0):
     """A DeviceSolver for a BASELINE config with U ~ 0.1 N(0,1) (seeded), other params at the
     reference init."""
-    cfg = CONFIGS[config] if isinstance(config, str) else config
+    cfg = get_config(config) if isinstance(config, str) else config
     arr = problem_arrays(cfg)
     eq = cfg["equation"].split("-")[0]
     eq = {"poisson_1d": "poisson", "allencahn_1d": "allencahn", "poisson_2d": "poisson",

@@ -172,6 +172,13 @@ int gpk_set_chain_capacity(int32_t workgroups);
 /* Tile workgroups per factor of the large-factor inverse's update launch (0: the default, two per
  * CU).  Applies to every later launch; tests use a few to give each workgroup long tile runs. */
 int gpk_set_spd_big_workgroups(int32_t workgroups);
+/* Poll budget of every inter-workgroup wait of later launches on the current device (polls > 0;
+ * 0 restores the default 2^22).  A wait that spends it -- a hand-off that never arrives, e.g. a
+ * persistent grid that is not co-resident -- gives up instead of hanging the device, and every
+ * other wait of the handle then gives up within 64 polls: the call returns GPK_ENOTPD ("hand-off
+ * timed out") and a gpk_step batch is undone (see gpk_step).  Tests force that path with 1 (every
+ * wait whose first poll fails gives up). */
+int gpk_set_wait_limit(int32_t polls);
 
 /* Graph selection state (see GPK_FLAG_NO_FAST_GRAPH): *fast = 1 if the next gpk_step uses the
  * fast graph, *rollbacks = batches rerun with the full graph so far.  Either pointer may be NULL. */
@@ -210,7 +217,10 @@ int gpk_loss_grad(gpk_handle* h, double* loss, double* grad_flat);
  * BEFORE each update (as step() returns it); may be NULL.  Returns once the losses and the
  * device status of the call are final: the last step's U update may still be running, like
  * the reference's asynchronously dispatched jax step; every later call on the handle is ordered
- * after it, and gpk_sync waits for it. */
+ * after it, and gpk_sync waits for it.  A batch (the whole call, or one 64-step chunk of the fast
+ * graph) that fails on the device -- GPK_ENOTPD: a non-positive pivot or a hand-off timeout --
+ * is undone: params, Adam state and step count are restored from the snapshot the batch took at
+ * its start (earlier chunks of the call stay applied, their losses written). */
 int gpk_step(gpk_handle* h, int32_t n_steps, double* losses);
 
 /* Wait until every launch enqueued on the handle has finished (timing). */

@@ -59,7 +59,11 @@ def test_sharded_section_ok_exits_zero():
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
-    assert "dry-run" in out["sharded"]
+    d = out["sharded"]["dry-run"]
+    # every sharded entry carries the same problem's single-GPU time (rank 0, same run) and the
+    # strong-scaling speedup over it
+    assert d["single_gpu_ms_per_step"] > 0 and d["speedup_vs_1gpu"] > 0, d
+    assert abs(d["speedup_vs_1gpu"] - d["single_gpu_ms_per_step"] / d["ms_per_step"]) < 1e-9
 
 
 @pytest.mark.parametrize("mode", ["hang", "raise"])

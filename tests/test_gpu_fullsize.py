@@ -146,16 +146,31 @@ def test_capped_capacity_falls_back_to_sweeps(capped_chain, eq, n1, n2):
     _cmp_lossgrad(prob, params, 8, fs, extended=(n1 < 200))
 
 
-def test_rank_group_never_uses_the_chain():
+def test_rank_group_chain_only_when_co_resident():
     """In-process rank groups launch concurrently on one device from several host threads: their
-    handles use the per-sweep inverse whatever the size."""
+    handles use the persistent chain only when every rank's chain grid fits the device together
+    (nranks x grid <= the co-resident capacity), else the per-sweep inverse.  A one-process-per-GPU
+    RCCL rank only needs its own grid to fit."""
+    from gpk.core import set_chain_capacity
     from tests.test_shard import _group
-    prob, params, _, fs = problem_2d(n1=64, n2=64, Q=4, seed=1)
+    prob, params, _, fs = problem_2d(n1=64, n2=64, Q=4, seed=1)   # P = 96 at 3 ranks: 20 workgroups
     g = _group(prob, 4, fs, 3)
     try:
-        assert g.inverse_path() == "sweep"
+        assert g.inverse_path() == "chain"
     finally:
         g.close()
+    set_chain_capacity(50)                 # one grid fits, three do not
+    try:
+        g = _group(prob, 4, fs, 3)
+        s = device_solver(prob, 4, fs)
+        try:
+            assert g.inverse_path() == "sweep"
+            assert s.inverse_path() in ("chain", "chain_aug")
+        finally:
+            g.close()
+            s.close()
+    finally:
+        set_chain_capacity(0)
 
 
 @pytest.mark.parametrize("n1,n2", [(3072, 3072), (4096, 4096)])

@@ -93,6 +93,41 @@ def test_group_eight_ranks_c4_size():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cid", ["C3", "C4"])
+def test_group_chain_path_two_ranks(cid):
+    """The exact per-rank path of an 8-GPU RCCL run (one process per GPU: the persistent chain
+    inverse + row-sharded GEMM descriptors + collectives), on one device: a 2-rank in-process
+    group whose two chain grids are co-resident takes the chain (gpk_inverse_path), and its loss /
+    full gradient match the oracle and its 10-step Adam trajectory the unsharded handle, at the
+    BASELINE configs C3 (128^2 SE_Cos) and C4 (256^2, the headline)."""
+    from tests.test_gpu_fullsize import _config_problem
+    prob, params, _, cfg = _config_problem(cid)
+    fs = cfg["freq_scale"]
+    g = _group(prob, 30, fs, 2)
+    s = device_solver(prob, 30, fs, flags=NO_AUG)
+    try:
+        assert g.inverse_path() == "chain", g.inverse_path()
+        assert g.shard_info()[1] == 2
+        g.set_params(params)
+        s.set_params(params)
+        lg, gg = g.loss_grad()
+        ls, gs = s.loss_grad()
+        lo, go = O.loss_grad_2d(prob, params)
+        tol = _tol(prob, params)
+        assert abs(lg - lo) / abs(lo) < tol, (lg, lo)
+        gd = O.unflatten_params(params, gg)
+        for k in go:
+            assert rel(O.flatten_params(gd[k]), O.flatten_params(go[k])) < tol, k
+        assert abs(lg - ls) / abs(ls) < 1e-11
+        assert rel(gg, gs) < 1e-9
+        assert rel(g.step(10), s.step(10)) < 1e-10
+        assert rel(g.get_flat(), s.get_flat()) < 1e-9
+    finally:
+        g.close()
+        s.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nranks,flags", [(2, 0), (4, 0), (2, 8)])
 def test_group_trajectory_matches_unsharded(nranks, flags):
     """10 Adam steps of the sharded group == 10 steps of one handle (params, losses); flags 8
