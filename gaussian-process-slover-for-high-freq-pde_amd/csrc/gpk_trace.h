@@ -44,6 +44,9 @@ enum TraceSlot {
   // items [first start, last end]
   SLOT_BIG_START = 240, SLOT_BIG_PIVTILE = 241, SLOT_BIG_PIVOT = 242, SLOT_BIG_PANEL_WAIT = 243,
   SLOT_BIG_PANEL = 244, SLOT_BIG_ROUND0 = 245, SLOT_BIG_ROUND1 = 246, SLOT_BIG_QUARTER = 247,
+  // rounds 0 and 1 of the tile workgroups (+ 3 j): [first, last] start, first K-step's MFMAs done
+  // (the base loads waited for), K-loop done (before the stores)
+  SLOT_BIG_R0START = 248,
 };
 constexpr int BIG_PROBE_SWEEP = 8;
 

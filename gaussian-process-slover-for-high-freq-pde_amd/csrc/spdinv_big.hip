@@ -69,38 +69,6 @@ struct BigSpdBatch {
 
 __device__ __forceinline__ int bw(int p, int I) { return min(BW, p - BW * I); }
 
-// 16x16 block of a 32-deep product out of LDS: acc += A(i0.., k) * B(k, j0..)
-// element (i,k) of A at a[i*sai + k*sak], (k,j) of B at b[k*sbk + j*sbj]
-__device__ __forceinline__ d4 mma16(const double* a, int sai, int sak, const double* b, int sbk,
-                                    int sbj, int i0, int j0, int lane, d4 acc) {
-  const int li = lane & 15, lk = lane >> 4;
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    const int k = 4 * kk + lk;
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[(i0 + li) * sai + k * sak],
-                                               b[k * sbk + (j0 + li) * sbj], acc, 0, 0, 0);
-  }
-  return acc;
-}
-
-// this wave's 32x32 quadrant (wr, wc) of a 64x64x64 product out of LDS (2x2 blocks of 16x16):
-// element (32wr + 16bi + (lane>>4) + 4r, 32wc + 16bj + (lane&15)) in acc[bi][bj][r]
-__device__ __forceinline__ void mm64(const double* a, int sai, int sak, const double* b, int sbk, int sbj,
-                                     int wr, int wc, int lane, d4 (&acc)[2][2]) {
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int k0 = 0; k0 < 64; k0 += 32)
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-        acc[bi][bj] = mma16(a + k0 * sak, sai, sak, b + k0 * sbk, sbk, sbj, 32 * wr + 16 * bi,
-                            32 * wc + 16 * bj, lane, acc[bi][bj]);
-}
-
 // S[r][c] = src[r*ld + c] for r < h, c < w (else 0): 64x64 tile, all 16 loads per thread in
 // flight before the LDS stores (one wave per row: coalesced)
 __device__ __forceinline__ void load_tile(double* S, const double* src, int ld, int h, int w, int t) {
@@ -115,19 +83,6 @@ __device__ __forceinline__ void load_tile(double* S, const double* src, int ld, 
   for (int q = 0; q < 16; ++q) S[(r0 + 4 * q) * SS + c] = v[q];
 }
 
-// S[r][c] = src[c*ld + r] (r < h, c < w; else 0): transposed 64x64 tile, reads along r
-__device__ __forceinline__ void load_tile_t(double* S, const double* src, int ld, int h, int w, int t) {
-  double v[16];
-  const int r = t & 63, c0 = t >> 6;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int c = c0 + 4 * q;
-    v[q] = (r < h && c < w) ? src[(size_t)c * ld + r] : 0.0;
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) S[r * SS + c0 + 4 * q] = v[q];
-}
-
 // the 32-pivot factorisation with its 8 block steps kept as a loop: inlined, it stays within
 // the update kernel's two-waves-per-SIMD register budget (a call costs the ABI's saved
 // registers: 277 VGPR + AGPR, one wave per SIMD)
@@ -135,163 +90,117 @@ __device__ __forceinline__ double pivot32(double* A, double* M, double* pv, int 
   return pivot_chol_inv_block<4, double*, NoPivotHook, 1>(A, M, pv, t, status);
 }
 
-// Factor the w x w (w = 32 or 64) SPD block at src (leading dimension ld; both triangles valid):
-// writes its L^{-1} as a 64x64 block at Li (leading dimension ldl, zero-padded), ldet2[0..1]
-// (one entry per 32 rows), status.  One 256-thread workgroup; sm >= PIVOT_LDS doubles.
-__device__ __forceinline__ void pivot64(const double* src, int ld, int w, double* Li, int ldl, double* ldet2,
-                        int* status, double* sm) {
-  double* S = sm;                   // [64][SS]
-  double* A = S + 64 * SS;          // [32][SP] factor scratch, then W
-  double* M1 = A + 32 * SP;         // [32][SP]
-  double* M2 = M1 + 32 * SP;        // [32][SP]
-  double* V = M2 + 32 * SP;         // [32][SP]
-  double* pv = V + 32 * SP;         // [32]
+// acc (16x16 block at rows i0, columns j0) += sa * A B over k < 32, A and B in LDS:
+// A(i, k) at a[i * sai + k * sak], B(k, j) at b[k * sbk + j * sbj]
+__device__ __forceinline__ d4 mma16s(const double* a, int sai, int sak, const double* b, int sbk, int sbj,
+                                     int i0, int j0, int lane, double sa, d4 acc) {
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const int k = 4 * kk + lk;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sa * a[(i0 + li) * sai + k * sak], b[k * sbk + (j0 + li) * sbj],
+                                               acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+constexpr int PB = SP;  // 32x32 LDS block stride (doubles)
+
+// ---- the pivot: blocked Cholesky of the sweep's w x w diagonal block (w <= W = 64 R) -------
+// Right-looking over 32-row blocks i: M_i = L_ii^{-1} (pivot32: Cholesky + L^{-1} of the 32x32
+// block), L_ji = A_ji M_i^T for the blocks below, A_jk -= L_ji L_ki^T on the trailing lower
+// blocks.  Output Lg (W x W, ld W): the strictly-lower blocks L_ji and, in the diagonal block
+// slots, M_i -- exactly what the panel's forward substitution reads (L_ii itself is never
+// needed, and L^{-1} of the whole block is never formed).  The trailing blocks live in the
+// scratch Sg = Lg + W^2 (this workgroup's own stores, read back after a drain + barrier).
+// Why this form (tools/gj_accuracy.py, C5's 4096^2 factors vs the long-double inverse): with the
+// forward-substitution panel below, a W-wide sweep does the 32-wide sweep's arithmetic -- K^{-1}
+// 1.38e-8 relative for W = 64 ... 512 -- where the previous form (L^{-1} of the 64/128 block by
+// the recursion -L22^{-1} V^T L11^{-1}, applied as one product) reached 3.4e-8 at W = 128, and
+// C5's dL/dU 1.0e-7 instead of 3.4e-8 (the fp64 LU oracle: 4.3e-8).
+template <int R>
+__device__ __forceinline__ void pivot_blk(const double* src, int ld, int w, double* Lg, double* ldet, int* status,
+                          double* sm) {
+  constexpr int W = BW * R;
+  double* Sg = Lg + W * W;
+  double* sP = sm;            // [32][PB] A_ii (clobbered by pivot32)
+  double* sM = sP + 32 * PB;  // [32][PB] M_i
+  double* pv = sM + 32 * PB;  // [32]
+  double* sL = pv + 32;       // [2R - 1][32][PB] A_ji, then L_ji (j > i)
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int wr = wv >> 1, wc = wv & 1;
-  load_tile(S, src, ld, w, w, t);
-  __syncthreads();
-  for (int e = t; e < 1024; e += 256) A[(e >> 5) * SP + (e & 31)] = S[(e >> 5) * SS + (e & 31)];
-  __syncthreads();
-  d4 acc;
-  const int ro = 16 * wr, co = 16 * wc;
-  double ls[2] = {0.0, 0.0};
-  // one copy of the (register-heavy) 32-pivot code: half h = 0 factors S11 (L^{-1} into M2, then
-  // moved to M1), h = 1 the Schur complement S22 - V^T V of the second half
+  const int li = lane & 15, lk = lane >> 4;
+  const int nb = w / 32;
 #pragma nounroll
-  for (int h = 0; h < w / 32; ++h) {
-    ls[h] = pivot32(A, M2, pv, t, status);
-    if (h == 0 && w == BW) {
-      for (int e = t; e < 32 * SP; e += 256) M1[e] = M2[e];
-      __syncthreads();
-      // V = M1 S12
-      acc = d4{0.0, 0.0, 0.0, 0.0};
-      acc = mma16(M1, SP, 1, S + 32, SS, 1, ro, co, lane, acc);
+  for (int i = 0; i < nb; ++i) {
+    const double* A = i == 0 ? src : Sg;  // (the trailing blocks: updated copies after step 0)
+    const int lda = i == 0 ? ld : W;
+    for (int e = t; e < 1024; e += 256)
+      sP[(e >> 5) * PB + (e & 31)] = A[(size_t)(32 * i + (e >> 5)) * lda + 32 * i + (e & 31)];
+#pragma nounroll
+    for (int q = 0; q < nb - 1 - i; ++q)
+      for (int e = t; e < 1024; e += 256)
+        sL[q * 32 * PB + (e >> 5) * PB + (e & 31)] = A[(size_t)(32 * (i + 1 + q) + (e >> 5)) * lda + 32 * i + (e & 31)];
+    __syncthreads();
+    const double ls = pivot32(sP, sM, pv, t, status);
+    if (t == 0) ldet[i] = ls;
+    for (int e = t; e < 1024; e += 256)
+      Lg[(size_t)(32 * i + (e >> 5)) * W + 32 * i + (e & 31)] = sM[(e >> 5) * PB + (e & 31)];
+    const int nl = nb - 1 - i;  // blocks below the pivot
+    if (nl == 0) break;
+    // L_ji = A_ji M_i^T (B(k, c) = M_i[c][k]); wave q computes j = i + 1 + q and overwrites its
+    // own A_ji in LDS with it (one wave's LDS operations are in order)
+    // (one 16x16 block at a time: the pivot is latency-bound, and inlined into the update kernel
+    // it must stay within that kernel's two-waves-per-SIMD register budget)
+    if (wv < nl) {
+      double* sA = sL + wv * 32 * PB;
+      const int j = i + 1 + wv;
+#pragma nounroll
+      for (int bi = 0; bi < 2; ++bi) {  // rows 16 bi.. of sA are read, then overwritten
+        d4 acc[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) V[(ro + (lane >> 4) + 4 * r) * SP + co + (lane & 15)] = acc[r];
-      __syncthreads();
-      // A = S22 - V^T V
-      acc = d4{0.0, 0.0, 0.0, 0.0};
-      acc = mma16(V, 1, SP, V, SP, 1, ro, co, lane, acc);
+        for (int bj = 0; bj < 2; ++bj)
+          acc[bj] = mma16s(sA, PB, 1, sM, 1, PB, 16 * bi, 16 * bj, lane, 1.0, d4{0.0, 0.0, 0.0, 0.0});
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = ro + (lane >> 4) + 4 * r, j = co + (lane & 15);
-        A[i * SP + j] = S[(32 + i) * SS + 32 + j] - acc[r];
+        for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * bi + lk + 4 * r, col = 16 * bj + li;
+            Lg[(size_t)(32 * j + row) * W + 32 * i + col] = acc[bj][r];
+            sA[row * PB + col] = acc[bj][r];
+          }
       }
-      __syncthreads();
     }
-  }
-  if (w != BW)
-    for (int e = t; e < 32 * SP; e += 256) M1[e] = M2[e];  // read after the barrier below
-  __syncthreads();
-  const double ls1 = ls[0], ls2 = ls[1];
-  if (w == BW) {
-    // A = W = V^T M1
-    acc = d4{0.0, 0.0, 0.0, 0.0};
-    acc = mma16(V, 1, SP, M1, SP, 1, ro, co, lane, acc);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) A[(ro + (lane >> 4) + 4 * r) * SP + co + (lane & 15)] = acc[r];
     __syncthreads();
-    // (L^{-1})_21 = -M2 W  -> S rows 32.., cols 0..31 (S is free now)
-    acc = d4{0.0, 0.0, 0.0, 0.0};
-    acc = mma16(M2, SP, 1, A, SP, 1, ro, co, lane, acc);
+    // trailing lower blocks (j, k), i < k <= j: A_jk -= L_ji L_ki^T (B(x, c) = L_ki[c][x])
+    const int nt = nl * (nl + 1) / 2;
+#pragma nounroll
+    for (int q = wv; q < nt; q += 4) {
+      int jj = 0;
+      while ((jj + 1) * (jj + 2) / 2 <= q) ++jj;
+      const int kk = q - jj * (jj + 1) / 2;
+      const int j = i + 1 + jj, k = i + 1 + kk;
+#pragma nounroll
+      for (int qb = 0; qb < 4; ++qb) {
+        const int bi = qb >> 1, bj = qb & 1;
+        d4 acc;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) S[(32 + ro + (lane >> 4) + 4 * r) * SS + co + (lane & 15)] = -acc[r];
+        for (int r = 0; r < 4; ++r) acc[r] = A[(size_t)(32 * j + 16 * bi + lk + 4 * r) * lda + 32 * k + 16 * bj + li];
+        acc = mma16s(sL + jj * 32 * PB, PB, 1, sL + kk * 32 * PB, 1, PB, 16 * bi, 16 * bj, lane, -1.0, acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Sg[(size_t)(32 * j + 16 * bi + lk + 4 * r) * W + 32 * k + 16 * bj + li] = acc[r];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-  }
-  for (int e = t; e < BW * BW; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    double v = 0.0;
-    if (r < 32 && c < 32) v = M1[r * SP + c];
-    else if (r >= 32 && r < w && c < 32) v = S[r * SS + c];
-    else if (r >= 32 && r < w && c >= 32 && c < w) v = M2[(r - 32) * SP + c - 32];
-    Li[r * ldl + c] = v;
-  }
-  if (t == 0) {
-    ldet2[0] = ls1;
-    if (w == BW) ldet2[1] = ls2;
   }
 }
 
-constexpr int PIVOT_LDS = 64 * SS + 4 * 32 * SP + 32;  // doubles
-
-// Factor the w x w (w <= 128) diagonal block at src: L^{-1} as a 128x128 block at Li (ld 128,
-// zero upper / padding), ldet4[0..3], status.  Li + 128*128 holds two 64x64 scratch blocks (the
-// Schur complement, V).  Every intermediate goes through global memory (this workgroup's own
-// writes, read back after a barrier: one L1 per workgroup), so the LDS need is pivot64's.
-//   L11^{-1} = chol_inv(S11);  V = L11^{-1} S12;  L22^{-1} = chol_inv(S22 - V^T V);
-//   (L^{-1})_21 = -L22^{-1} (V^T L11^{-1})
-__device__ __forceinline__ void pivot128(const double* src, int ld, int w, double* Li, double* ldet4, int* status,
-                         double* sm) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int wr = wv >> 1, wc = wv & 1;
-  double* Sg = Li + 128 * 128;  // [64][64] Schur complement
-  double* Vg = Sg + 64 * 64;    // [64][64] V
-  const int w1 = min(BW, w), w2 = w - BW;
-  pivot64(src, ld, w1, Li, 128, ldet4, status, sm);
-  __syncthreads();
-  if (w2 <= 0) return;  // (the last, <= 64 wide sweep reads the L11 block only)
-  double* sA = sm;
-  double* sB = sm + 64 * SS;
-  d4 acc[2][2];
-  // V = L11^{-1} S12  (columns >= w2 are zero); S12 = S21^T from the lower storage (during the
-  // sweeps only the lower tiles are current)
-  load_tile(sA, Li, 128, BW, BW, t);
-  load_tile_t(sB, src + (size_t)BW * ld, ld, BW, w2, t);
-  __syncthreads();
-  mm64(sA, SS, 1, sB, SS, 1, wr, wc, lane, acc);
-  __syncthreads();
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 32 * wr + 16 * bi + (lane >> 4) + 4 * r, j = 32 * wc + 16 * bj + (lane & 15);
-        sA[i * SS + j] = acc[bi][bj][r];
-        Vg[i * 64 + j] = acc[bi][bj][r];
-      }
-  __syncthreads();
-  // Schur complement S22 - V^T V -> Sg
-  mm64(sA, 1, SS, sA, SS, 1, wr, wc, lane, acc);
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 32 * wr + 16 * bi + (lane >> 4) + 4 * r, j = 32 * wc + 16 * bj + (lane & 15);
-        if (i < w2 && j < w2) Sg[i * 64 + j] = src[(size_t)(BW + i) * ld + BW + j] - acc[bi][bj][r];
-      }
-  __syncthreads();
-  pivot64(Sg, 64, w2, Li + BW * 128 + BW, 128, ldet4 + 2, status, sm);
-  __syncthreads();
-  // W = V^T L11^{-1}, then (L^{-1})_21 = -L22^{-1} W
-  load_tile(sA, Vg, 64, BW, BW, t);
-  load_tile(sB, Li, 128, BW, BW, t);
-  __syncthreads();
-  mm64(sA, 1, SS, sB, SS, 1, wr, wc, lane, acc);
-  __syncthreads();
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        sA[(32 * wr + 16 * bi + (lane >> 4) + 4 * r) * SS + 32 * wc + 16 * bj + (lane & 15)] = acc[bi][bj][r];
-  load_tile(sB, Li + BW * 128 + BW, 128, BW, BW, t);
-  __syncthreads();
-  mm64(sB, SS, 1, sA, SS, 1, wr, wc, lane, acc);
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 32 * wr + 16 * bi + (lane >> 4) + 4 * r, j = 32 * wc + 16 * bj + (lane & 15);
-        Li[(BW + i) * 128 + j] = -acc[bi][bj][r];
-        Li[i * 128 + BW + j] = 0.0;  // upper-right block
-      }
-}
+template <int R>
+constexpr int pivot_lds() { return 2 * 32 * PB + 32 + (2 * R - 1) * 32 * PB; }
+// the panel: X_i (32 x 65) + one row block of L (2R blocks of 32 x PB)
+template <int R>
+constexpr int panel_lds() { return 32 * 65 + 2 * R * 32 * PB; }
+constexpr int PIVOT_LDS = pivot_lds<2>() > panel_lds<2>() ? pivot_lds<2>() : panel_lds<2>();  // doubles
 
 // the panel buffer of sweep k (the update of sweep k reads it while the panel of sweep k + 1 is
 // written into the other one, by the same launch)
@@ -318,16 +227,12 @@ __device__ __forceinline__ void acquire_wait(const unsigned int* c, unsigned int
   __syncthreads();
 }
 
-// the pivot block of sweep k: 64-pivot (R = 1) or 128-pivot (R = 2)
+// the pivot block of sweep k (W = 64 R rows): L and the M_i into Li, log det per 32 rows
 template <int R>
 __device__ __forceinline__ void pivot_block(const BigSpdBatch& b, int m, int k, double* sm) {
   const int p = b.p[m];
   const int r0 = BW * R * k, w = min(BW * R, p - r0);
-  const double* src = b.X[m] + (size_t)r0 * p + r0;
-  if (R == 1)
-    pivot64(src, p, w, b.Li[m], BW, b.ldet[m] + 2 * k, b.status[m], sm);
-  else
-    pivot128(src, p, w, b.Li[m], b.ldet[m] + 4 * k, b.status[m], sm);
+  pivot_blk<R>(b.X[m] + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 2 * R * k, b.status[m], sm);
 }
 
 template <int R>
@@ -345,73 +250,96 @@ __global__ __launch_bounds__(256) void big_pivot_init_kernel(BigSpdBatch b) {
   }
 }
 
-// Row block rh (64 rows) of the panel Z[:, J-block] = L^{-1} X_{P,J} (X_{P,J} of the lower
-// storage: row block P for J < P, the transpose of column block P for J > P); Z[:, P-block] =
-// L^{-1}.  L^{-1} is lower triangular: row block rh sums the column blocks kh <= rh.
-// One 256-thread workgroup, LDS sm >= 2 x 64 x 65 doubles; into zbuf(k).
+// ---- the panel: Z_{:,J} = L^{-1} X_{P,J} by forward substitution over 32-row blocks ---------
+// One 256-thread workgroup per 64 columns J of the factor (J < T; the last tile may be 32 wide).
+// Stage i: acc = X_i - sum_{j<i} L_ij Z_j, then Z_i = M_i acc (X_i: rows 32 i.. of X_{P,J} in
+// the lower storage -- row block P for J < P, the transpose of column block P for J > P -- and
+// the identity for the sweep's own columns, whose Z is L^{-1} itself).  Wave w owns columns
+// 16 w.. of the block for every row, so each Z_j stays in its registers: a 16x16 MFMA result in
+// the C layout (element (lk + 4 r, li) in acc[r]) is the B operand of the next product's k-steps
+// (k-step r reads B[4 r + lk][li]).  Row block i of Lg (L_i0 .. L_i,i-1, M_i) is staged in LDS.
 template <int R>
-__device__ void panel_block(const BigSpdBatch& b, int m, int k, int J, int rh, double* sm) {
+__device__ __forceinline__ void panel_block(const BigSpdBatch& b, int m, int k, int J, double* sm) {
+  constexpr int NB = 2 * R;
   const int p = b.p[m], T = b.T[m];
-  const int P0 = R * k;  // first tile of the swept block
+  const int P0 = R * k;  // first 64-tile of the swept block
   if (P0 >= T || J >= T) return;
-  const int w = min(BW * R, p - BW * P0);  // sweep width
-  if (BW * rh >= w) return;
-  const int hr = min(BW, w - BW * rh);     // rows of this output block
-  const int ldl = BW * R;
+  const int nb = min(BW * R, p - BW * P0) / 32;
+  const int r0 = BW * P0, c0 = BW * J, wJ = bw(p, J);
+  const bool own = J >= P0 && J < P0 + R;
   const double* X = b.X[m];
+  const double* Lg = b.Li[m];
   double* Z = zbuf<R>(b, m, k);
-  const double* Li = b.Li[m];
+  double* sX = sm;            // [32][65]
+  double* sL = sm + 32 * 65;  // [NB][32][PB]
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int wJ = bw(p, J);
-  if (J >= P0 && J < P0 + R) {
-    const int jc = J - P0;
-    for (int e = t; e < BW * BW; e += 256) {
-      const int r = e >> 6, c = e & 63;
-      if (r < hr && c < wJ) Z[(size_t)(BW * rh + r) * p + BW * J + c] = Li[(BW * rh + r) * ldl + BW * jc + c];
-    }
-    return;
-  }
-  double* sL = sm;
-  double* sX = sm + BW * SS;
-  const int wr = wv >> 1, wc = wv & 1;
-  d4 acc[2][2];
+  const int li = lane & 15, lk = lane >> 4;
+  const int col = c0 + 16 * wv + li;
+  d4 z[NB][2];
 #pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj) acc[bi][bj] = d4{0.0, 0.0, 0.0, 0.0};
-  for (int kh = 0; kh <= rh; ++kh) {
-    const int wk = min(BW, w - BW * kh);
-    const int I = P0 + kh;
-    if (kh) __syncthreads();
-    load_tile(sL, Li + (size_t)(BW * rh) * ldl + BW * kh, ldl, BW, BW, t);
-    if (J < P0)  // row block I of the lower storage
-      load_tile(sX, X + (size_t)(BW * I) * p + BW * J, p, wk, wJ, t);
-    else         // tile (J, I): X_{I,J}[r][c] = X[J*64 + c][I*64 + r]
-      load_tile_t(sX, X + (size_t)(BW * J) * p + BW * I, p, wk, wJ, t);
-    __syncthreads();
-    for (int k0 = 0; k0 < wk; k0 += 32)
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj)
-          acc[bi][bj] = mma16(sL + k0, SS, 1, sX + k0 * SS, SS, 1, 32 * wr + 16 * bi, 32 * wc + 16 * bj,
-                              lane, acc[bi][bj]);
-  }
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 32 * wr + 16 * bi + (lane >> 4) + 4 * r, col = 32 * wc + 16 * bj + (lane & 15);
-        if (row < hr && col < wJ) Z[(size_t)(BW * rh + row) * p + BW * J + col] = acc[bi][bj][r];
+  for (int i = 0; i < NB; ++i) {
+    if (i >= nb) break;
+    if (i) __syncthreads();  // the previous stage's LDS reads are done
+    if (own) {
+      for (int e = t; e < 2048; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        sX[r * 65 + c] = (r0 + 32 * i + r == c0 + c) ? 1.0 : 0.0;
       }
+    } else if (J < P0) {
+      for (int e = t; e < 2048; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        sX[r * 65 + c] = c < wJ ? X[(size_t)(r0 + 32 * i + r) * p + c0 + c] : 0.0;
+      }
+    } else {  // X_{P,J}[r][c] = X[c0 + c][r0 + 32 i + r]: coalesced along r
+      for (int e = t; e < 2048; e += 256) {
+        const int r = e & 31, c = e >> 5;
+        sX[r * 65 + c] = c < wJ ? X[(size_t)(c0 + c) * p + r0 + 32 * i + r] : 0.0;
+      }
+    }
+    for (int e = t; e < 1024 * (i + 1); e += 256) {
+      const int q = e >> 10, r = (e >> 5) & 31, c = e & 31;
+      sL[q * 32 * PB + r * PB + c] = Lg[(size_t)(32 * i + r) * (BW * R) + 32 * q + c];
+    }
+    __syncthreads();
+    d4 acc[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[h][r] = sX[(16 * h + lk + 4 * r) * 65 + 16 * wv + li];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (j >= i) break;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(-sL[j * 32 * PB + (16 * h + li) * PB + 16 * hh + 4 * kk + lk],
+                                                          z[j][hh][kk], acc[h], 0, 0, 0);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      z[i][h] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          z[i][h] = __builtin_amdgcn_mfma_f64_16x16x4f64(sL[i * 32 * PB + (16 * h + li) * PB + 16 * hh + 4 * kk + lk],
+                                                         acc[hh][kk], z[i][h], 0, 0, 0);
+    }
+    if (col < p)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Z[(size_t)(32 * i + 16 * h + lk + 4 * r) * p + col] = z[i][h][r];
+  }
 }
 
 template <int R>
 __global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
-  __shared__ double sm[2 * BW * SS];
-  panel_block<R>(b, blockIdx.y, k, blockIdx.x / R, blockIdx.x % R, sm);
+  __shared__ double sm[PIVOT_LDS];
+  panel_block<R>(b, blockIdx.y, k, blockIdx.x, sm);
 }
 
 // The next sweep's panel, fused into the update launch of sweep k (its last workgroups): it
@@ -423,7 +351,7 @@ __device__ void fused_panel(const BigSpdBatch& b, int m, int k, int pj, unsigned
   const unsigned int* fl = b.flag[m];
   acquire_wait(fl + 1, (unsigned)(k + 1), b.status[m]);
   acquire_wait(fl + 2, (unsigned)(k + 1) * row_tiles, b.status[m]);
-  panel_block<R>(b, m, k + 1, pj / R, pj % R, sm);
+  panel_block<R>(b, m, k + 1, pj, sm);
 }
 
 __device__ __forceinline__ void tile_of(int lin, int& I, int& J) {
@@ -721,7 +649,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // and applies the sweep's epilogue (sign, zero base in the swept row / column).  Diagonal tiles
 // keep both triangles of their 128 block, so every lower 64-tile the panel reads is current.
 // Workgroup 0 of a factor owns the next pivot block's tile (k+1, k+1): it updates it like the
-// others, then factors it in place (pivot128: Cholesky + L^{-1}) while the other tiles are
+// others, then factors it in place (pivot_blk: blocked Cholesky) while the other tiles are
 // updated -- no hand-off, no workgroup waits on another.  The last sweep flips the sign and
 // publishes max diag K^{-1}; big_mirror_kernel then fills the upper triangle.
 constexpr int WT = 128;
@@ -748,11 +676,11 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   if (L >= 8 * nx + 8) {  // the next sweep's panel (fused_panel)
     const int tmax = max(b.T[0], b.nmat > 1 ? b.T[1] : 0);
     const int pi = L - 8 * nx - 8;
-    const int m = pi / (2 * tmax);
-    const int pj = pi % (2 * tmax);
+    const int m = pi / tmax;
+    const int pj = pi % tmax;  // 64 columns per panel workgroup
     if (m >= b.nmat) return;
     const int T2 = (b.p[m] + WT - 1) / WT;
-    if (k + 1 >= T2 || skip_pivot || pj >= 2 * b.T[m]) return;
+    if (k + 1 >= T2 || skip_pivot || pj >= b.T[m]) return;
     // T2 - 1 panel-row tiles per sweep, counted in quarter tiles (a whole tile adds 4)
     if (probe && m == 0) TR_LO(SLOT_BIG_PANEL_WAIT);
     fused_panel<2>(b, m, k, pj, 4u * (unsigned)(T2 - 1), sm);
@@ -819,6 +747,10 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   if (qq < 0)
     fetch<1, 0>(R, zbuf<2>(b, m, k), b.p[m], zbuf<2>(b, m, k), b.p[m], b.p[m], b.p[m], WT * ti, WT * tj, 0, t);
   for (; qq < 0; ++j) {
+    if (probe && !pivot && j < 2) {  // (trace build) round-0/1 phases over every tile workgroup
+      TR_LO(SLOT_BIG_R0START + 3 * j);
+      TR_HI(SLOT_BIG_R0START + 3 * j);
+    }
     const int p = b.p[m];
     const int T2 = (p + WT - 1) / WT;  // 128-tiles per dimension
     const bool has_next = k + 1 < T2;
@@ -872,8 +804,10 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
         mma(sA0 + cur * SZ, sB0 + cur * SZ, wr, wc, lane, acc);
         if (kt + 1 < nk) store<1, 0>(R, sA0 + (cur ^ 1) * SZ, sB0 + (cur ^ 1) * SZ, -1.0, t);
         __syncthreads();
+        if (probe && !pivot && j < 2 && kt == 0) TR_HI(SLOT_BIG_R0START + 3 * j + 1);
       }
     }
+    if (probe && !pivot && j < 2) TR_HI(SLOT_BIG_R0START + 3 * j + 2);
     double mx = 0.0;
 #pragma unroll
     for (int bx = 0; bx < 4; ++bx) {
@@ -904,7 +838,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
       if (probe && m == 0) TR_HI(SLOT_BIG_PIVTILE);
       __syncthreads();
       const int r0 = WT * Q, w = min(WT, p - r0);
-      pivot128(X + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 4 * Q, b.status[m], sm);
+      pivot_blk<2>(X + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 4 * Q, b.status[m], sm);
       release_add(b.flag[m] + 1, 1u);  // L^{-1} of pivot k + 1 ready (fused_panel)
       if (probe && m == 0) TR_HI(SLOT_BIG_PIVOT);
       return;
@@ -1088,7 +1022,7 @@ void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int sta
   if (stage < 0) {
     hipLaunchKernelGGL(big_pivot_init_kernel<R>, dim3(nmat), dim3(256), 0, s, b);
   } else if ((stage & 1) == 0) {
-    hipLaunchKernelGGL(big_panel_kernel<R>, dim3(Tmax * R, nmat), dim3(256), 0, s, b, stage >> 1);
+    hipLaunchKernelGGL(big_panel_kernel<R>, dim3(Tmax, nmat), dim3(256), 0, s, b, stage >> 1);
   } else if (R == 1) {  // + the next sweep's panel workgroups (Tmax per factor)
     hipLaunchKernelGGL(big_update_kernel<1>, dim3(tiles + Tmax, nmat), dim3(256), 0, s, b, stage >> 1,
                        skip_pivot);
@@ -1101,7 +1035,7 @@ void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int sta
     const int nx = std::max(1, std::min(per_xcd, 2 * first / 8));
     const int tile_wgs = 8 * nx;
     const int fst = std::min(first, tile_wgs);  // (fewer tile workgroups than CUs: pivots right after)
-    hipLaunchKernelGGL(wide_update_kernel, dim3(tile_wgs + 8 + nmat * 2 * Tmax), dim3(256), 0, s, b, k,
+    hipLaunchKernelGGL(wide_update_kernel, dim3(tile_wgs + 8 + nmat * Tmax), dim3(256), 0, s, b, k,
                        skip_pivot, gx, per_xcd, nx, fst);
     // after the last sweep of every factor (a smaller factor's last sweep came earlier; later
     // launches leave it alone)
@@ -1114,7 +1048,8 @@ void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int sta
 
 int spd_big_sweeps(int p, int wide) { return (p + BW * (wide ? 2 : 1) - 1) / (BW * (wide ? 2 : 1)); }
 
-size_t spd_big_piv_doubles(int p) { return std::max<size_t>((size_t)p * 32, 128 * 128 + 2 * 64 * 64); }
+// the pivot's L + M_i (W x W) and its trailing-block scratch (W x W), W <= 128
+size_t spd_big_piv_doubles(int p) { return std::max<size_t>((size_t)p * 32, 2 * 128 * 128); }
 
 // stage -1: pivot 0; stage 2k: panel k (standalone; the inverse launches it for k = 0 only);
 // stage 2k+1: update k + the fused panel of sweep k + 1 (profiling / bench)

@@ -9,11 +9,13 @@ yardstick per key -- the reference algorithm's rounding error on these inputs.  
 above 2^20 elements (C5) keep a seeded sample of 16384 positions plus the full max-abs.
 
 Bar, per gradient key (max-abs error / max-abs value, tests/helpers.rel):
-    max(floor, 4 x the LU oracle's own distance from the yardstick)
+    max(floor, MULT x the LU oracle's own distance from the yardstick)
 with floor 1e-8 at the ill-conditioned C2 / C5 (cond(K) ~ 1e7-1e8) and 1e-10
 elsewhere.  At C5 the LU oracle itself is 4.3e-8 from the yardstick in dL/dU, so "within 1e-8 of
-the LU oracle" is not a meaningful bar there; the yardstick is.  Every observed error goes to
-the parity log (tests/helpers.record_parity -> profiles/r3_parity.json).
+the LU oracle" is not a meaningful bar there; the yardstick is.  MULT is 1 at C5 (round 4: the
+large-factor inverse does the 32-wide sweep's arithmetic, DESIGN.md §5, and the device is at
+least as accurate as the reference's own algorithm there) and 4 elsewhere.  Every observed error
+goes to the parity log (tests/helpers.record_parity -> profiles/r*_parity.json).
 
 Predictions (`preds`, the solution field, on the reference's M = 300 test grid at the same
 params): within 1e-6 relative L2 of the oracle's preds (the north star's figure).
@@ -29,6 +31,7 @@ from tests.helpers import config_problem, record_parity, rel
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 FLOOR = {"C1": 1e-10, "C2": 1e-8, "C3": 1e-10, "C4": 1e-10, "C5": 1e-8}
+MULT = {"C1": 4.0, "C2": 4.0, "C3": 4.0, "C4": 4.0, "C5": 1.0}
 
 
 def _fixture(cid):
@@ -46,10 +49,10 @@ def fixture_errors(fx, loss, gflat_by_key):
 
 
 def fixture_tol(fx, cid):
-    tol = {"loss": max(FLOOR[cid], 4 * float(fx["loss_lu_err"]))}
+    tol = {"loss": max(FLOOR[cid], MULT[cid] * float(fx["loss_lu_err"]))}
     for f in fx.files:
         if f.startswith("lu_err/"):
-            tol[f[7:]] = max(FLOOR[cid], 4 * float(fx[f]))
+            tol[f[7:]] = max(FLOOR[cid], MULT[cid] * float(fx[f]))
     return tol
 
 

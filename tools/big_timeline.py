@@ -11,7 +11,10 @@ from gpk import _lib, problems
 
 NAMES = {240: "launch start (wg 0)", 241: "pivot wg: start .. its tile done", 242: "pivot128 done",
          243: "panel wgs: first start", 244: "panel done (last)", 245: "tile wgs: round 0 done (max)",
-         246: "tile wgs: round 1 done (max)", 247: "quarter items: first start .. last end"}
+         246: "tile wgs: round 1 done (max)", 247: "quarter items: first start .. last end",
+         248: "round 0: tile start (first .. last wg)", 249: "round 0: first K-step done (last wg)",
+         250: "round 0: K-loop done (last wg)", 251: "round 1: tile start (first .. last wg)",
+         252: "round 1: first K-step done (last wg)", 253: "round 1: K-loop done (last wg)"}
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
 a = ap.parse_args()
