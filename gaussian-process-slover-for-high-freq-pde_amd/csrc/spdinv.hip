@@ -895,6 +895,10 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
   const size_t rs0 = std::min(ntot, (size_t)gidx * share), rs1 = std::min(ntot, rs0 + share);
   const size_t rchunk = (share + T - 1) / T;
 
+  __shared__ unsigned s_lword_;  // sweep k + 1 once thread 0 has seen a word of L_k^{-1}
+  volatile unsigned* s_lword = &s_lword_;
+  if (t == 0) *s_lword = 0u;
+  __syncthreads();
   // V slots: 0, 1 = rows 2R, 2R+1; 2, 3 = the plain column pair's columns 2c0, 2c0+1
   auto vslot_of_col = [&](int s) { return s < 4 ? 2 + (s & 1) : (s == 6 ? 1 : 0); };
   for (int k = 0; k < T && !master; ++k) {
@@ -962,16 +966,31 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
       for (int r = 0; r < 4; ++r) ok = ok && gran_ok(lv[r]);
       return ok;
     };
+    // L_k^{-1}: while the panel is awaited, thread 0 polls ONE of its words (a flag's polling
+    // traffic); once that word is in, every thread issues its own words with its next panel
+    // re-load, so they arrive under the panel wait instead of one round trip after it.  Polling
+    // all of L_k^{-1}'s words with the panel had ~500 workgroups re-loading the same 8 KB while
+    // the pivot was being factored (measured: C2 0.638 -> 0.676 ms), and so did loading them
+    // once with the panel's first attempt (0.614 -> 0.677 ms): no thread touches the slots
+    // before that one word is in.
     load_panel();
+    if (t == 0) lv[0] = ld_sc1(Li);  // (thread 0's first word is the one polled)
+    bool lissued = false;
     for (unsigned spins = 0; !panel_ok(); ++spins) {
       if (spin_give_up(spins, F.status)) break;
+      if (!lissued) {
+        if (t == 0 && gran_ok(lv[0])) *s_lword = k + 1;
+        if (*s_lword == (unsigned)(k + 1)) {
+          load_l();
+          lissued = true;
+        }
+      }
       __builtin_amdgcn_s_sleep(1);
       reload_panel();
+      if (t == 0 && !lissued) lv[0] = ld_sc1(Li);
     }
     if (trc) TR_HI(SLOT_MC_PANEL + k);
-    // L_k^{-1} only once the panel is in: polling both together had ~500 workgroups re-loading
-    // the same 8 KB while the pivot was being factored (measured: C2 0.638 -> 0.676 ms)
-    load_l();
+    load_l();  // (the words not yet loaded, or still holding the sentinel)
     for (unsigned spins = 0; !l_ok(); ++spins) {
       if (spin_give_up(spins, F.status)) break;
       __builtin_amdgcn_s_sleep(1);
