@@ -83,13 +83,6 @@ __device__ __forceinline__ void load_tile(double* S, const double* src, int ld, 
   for (int q = 0; q < 16; ++q) S[(r0 + 4 * q) * SS + c] = v[q];
 }
 
-// the 32-pivot factorisation with its 8 block steps kept as a loop: inlined, it stays within
-// the update kernel's two-waves-per-SIMD register budget (a call costs the ABI's saved
-// registers: 277 VGPR + AGPR, one wave per SIMD)
-__device__ __forceinline__ double pivot32(double* A, double* M, double* pv, int t, int* status) {
-  return pivot_chol_inv_block<4, double*, NoPivotHook, 1>(A, M, pv, t, status);
-}
-
 // acc (16x16 block at rows i0, columns j0) += sa * A B over k < 32, A and B in LDS:
 // A(i, k) at a[i * sai + k * sak], B(k, j) at b[k * sbk + j * sbj]
 __device__ __forceinline__ d4 mma16s(const double* a, int sai, int sak, const double* b, int sbk, int sbj,
@@ -107,12 +100,19 @@ __device__ __forceinline__ d4 mma16s(const double* a, int sai, int sak, const do
 constexpr int PB = SP;  // 32x32 LDS block stride (doubles)
 
 // ---- the pivot: blocked Cholesky of the sweep's w x w diagonal block (w <= W = 64 R) -------
-// Right-looking over 32-row blocks i: M_i = L_ii^{-1} (pivot32: Cholesky + L^{-1} of the 32x32
-// block), L_ji = A_ji M_i^T for the blocks below, A_jk -= L_ji L_ki^T on the trailing lower
-// blocks.  Output Lg (W x W, ld W): the strictly-lower blocks L_ji and, in the diagonal block
-// slots, M_i -- exactly what the panel's forward substitution reads (L_ii itself is never
-// needed, and L^{-1} of the whole block is never formed).  The trailing blocks live in the
-// scratch Sg = Lg + W^2 (this workgroup's own stores, read back after a drain + barrier).
+// Right-looking over 32-row blocks i: M_i = L_ii^{-1} (Cholesky + L^{-1} of the 32x32 block),
+// L_ji = A_ji M_i^T for the blocks below, A_jk -= L_ji L_ki^T on the trailing lower blocks.
+// Output Lg (W x W, ld W): the strictly-lower blocks L_ji and, in the diagonal block slots, M_i
+// -- exactly what the panel's forward substitution reads (L_ii itself is never needed, and L^{-1}
+// of the whole block is never formed).
+// Register-resident: wave (bi, bj) keeps the 16x16 quadrant (bi, bj) of every lower 32x32 block
+// in an MFMA accumulator for the whole factorisation (at most 10 blocks: 40 doubles per lane),
+// loaded with one batch of loads; a block step stages its diagonal block and the column below it
+// in LDS, factors the diagonal block on ONE wave (pivot_chol_inv_1w, bitwise the four-wave form),
+// forms L_ji in place, and every wave subtracts L_ji L_ki^T from its quadrants of the trailing
+// blocks -- no global round trip between block steps (the previous form kept the trailing blocks
+// in a global scratch and loaded each 16x16 block's base just before its MFMAs: 46 us per
+// 128-pivot).  Same products in the same order: bitwise that form.
 // Why this form (tools/gj_accuracy.py, C5's 4096^2 factors vs the long-double inverse): with the
 // forward-substitution panel below, a W-wide sweep does the 32-wide sweep's arithmetic -- K^{-1}
 // 1.38e-8 relative for W = 64 ... 512 -- where the previous form (L^{-1} of the 64/128 block by
@@ -120,28 +120,38 @@ constexpr int PB = SP;  // 32x32 LDS block stride (doubles)
 // C5's dL/dU 1.0e-7 instead of 3.4e-8 (the fp64 LU oracle: 4.3e-8).
 template <int R>
 __device__ __forceinline__ void pivot_blk(const double* src, int ld, int w, double* Lg, double* ldet, int* status,
-                          double* sm) {
-  constexpr int W = BW * R;
-  double* Sg = Lg + W * W;
-  double* sP = sm;            // [32][PB] A_ii (clobbered by pivot32)
+                                          double* sm) {
+  constexpr int W = BW * R, NB = 2 * R;
+  double* sP = sm;            // [32][PB] A_ii (clobbered by the factorisation)
   double* sM = sP + 32 * PB;  // [32][PB] M_i
   double* pv = sM + 32 * PB;  // [32]
-  double* sL = pv + 32;       // [2R - 1][32][PB] A_ji, then L_ji (j > i)
+  double* sL = pv + 32;       // [NB - 1][32][PB] A_ji, then L_ji (j > i)
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int li = lane & 15, lk = lane >> 4;
+  const int bi = wv >> 1, bj = wv & 1;  // this wave's quadrant of every block
   const int nb = w / 32;
-#pragma nounroll
-  for (int i = 0; i < nb; ++i) {
-    const double* A = i == 0 ? src : Sg;  // (the trailing blocks: updated copies after step 0)
-    const int lda = i == 0 ? ld : W;
-    for (int e = t; e < 1024; e += 256)
-      sP[(e >> 5) * PB + (e & 31)] = A[(size_t)(32 * i + (e >> 5)) * lda + 32 * i + (e & 31)];
-#pragma nounroll
-    for (int q = 0; q < nb - 1 - i; ++q)
-      for (int e = t; e < 1024; e += 256)
-        sL[q * 32 * PB + (e >> 5) * PB + (e & 31)] = A[(size_t)(32 * (i + 1 + q) + (e >> 5)) * lda + 32 * i + (e & 31)];
+  d4 a[NB][NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int k = 0; k <= j; ++k)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        a[j][k][r] = j < nb ? src[(size_t)(32 * j + 16 * bi + lk + 4 * r) * ld + 32 * k + 16 * bj + li] : 0.0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    if (i >= nb) break;
+    if (i) __syncthreads();  // the previous step's trailing products are done reading sL
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * bi + lk + 4 * r, col = 16 * bj + li;
+      sP[row * PB + col] = a[i][i][r];
+#pragma unroll
+      for (int j = i + 1; j < NB; ++j)
+        if (j < nb) sL[(j - i - 1) * 32 * PB + row * PB + col] = a[j][i][r];
+    }
     __syncthreads();
-    const double ls = pivot32(sP, sM, pv, t, status);
+    const double ls = pivot_chol_inv_1w(sP, sM, pv, t, status);
     if (t == 0) ldet[i] = ls;
     for (int e = t; e < 1024; e += 256)
       Lg[(size_t)(32 * i + (e >> 5)) * W + 32 * i + (e & 31)] = sM[(e >> 5) * PB + (e & 31)];
@@ -149,50 +159,37 @@ __device__ __forceinline__ void pivot_blk(const double* src, int ld, int w, doub
     if (nl == 0) break;
     // L_ji = A_ji M_i^T (B(k, c) = M_i[c][k]); wave q computes j = i + 1 + q and overwrites its
     // own A_ji in LDS with it (one wave's LDS operations are in order)
-    // (one 16x16 block at a time: the pivot is latency-bound, and inlined into the update kernel
-    // it must stay within that kernel's two-waves-per-SIMD register budget)
     if (wv < nl) {
       double* sA = sL + wv * 32 * PB;
       const int j = i + 1 + wv;
 #pragma nounroll
-      for (int bi = 0; bi < 2; ++bi) {  // rows 16 bi.. of sA are read, then overwritten
+      for (int hb = 0; hb < 2; ++hb) {  // rows 16 hb.. of sA are read, then overwritten
         d4 acc[2];
 #pragma unroll
-        for (int bj = 0; bj < 2; ++bj)
-          acc[bj] = mma16s(sA, PB, 1, sM, 1, PB, 16 * bi, 16 * bj, lane, 1.0, d4{0.0, 0.0, 0.0, 0.0});
+        for (int hc = 0; hc < 2; ++hc)
+          acc[hc] = mma16s(sA, PB, 1, sM, 1, PB, 16 * hb, 16 * hc, lane, 1.0, d4{0.0, 0.0, 0.0, 0.0});
 #pragma unroll
-        for (int bj = 0; bj < 2; ++bj)
+        for (int hc = 0; hc < 2; ++hc)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int row = 16 * bi + lk + 4 * r, col = 16 * bj + li;
-            Lg[(size_t)(32 * j + row) * W + 32 * i + col] = acc[bj][r];
-            sA[row * PB + col] = acc[bj][r];
+            const int row = 16 * hb + lk + 4 * r, col = 16 * hc + li;
+            Lg[(size_t)(32 * j + row) * W + 32 * i + col] = acc[hc][r];
+            sA[row * PB + col] = acc[hc][r];
           }
       }
     }
     __syncthreads();
     // trailing lower blocks (j, k), i < k <= j: A_jk -= L_ji L_ki^T (B(x, c) = L_ki[c][x])
-    const int nt = nl * (nl + 1) / 2;
-#pragma nounroll
-    for (int q = wv; q < nt; q += 4) {
-      int jj = 0;
-      while ((jj + 1) * (jj + 2) / 2 <= q) ++jj;
-      const int kk = q - jj * (jj + 1) / 2;
-      const int j = i + 1 + jj, k = i + 1 + kk;
-#pragma nounroll
-      for (int qb = 0; qb < 4; ++qb) {
-        const int bi = qb >> 1, bj = qb & 1;
-        d4 acc;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = A[(size_t)(32 * j + 16 * bi + lk + 4 * r) * lda + 32 * k + 16 * bj + li];
-        acc = mma16s(sL + jj * 32 * PB, PB, 1, sL + kk * 32 * PB, 1, PB, 16 * bi, 16 * bj, lane, -1.0, acc);
+    for (int j = i + 1; j < NB; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Sg[(size_t)(32 * j + 16 * bi + lk + 4 * r) * W + 32 * k + 16 * bj + li] = acc[r];
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+      for (int k = i + 1; k <= j; ++k)
+        if (j < nb)
+          a[j][k] = mma16s(sL + (j - i - 1) * 32 * PB, PB, 1, sL + (k - i - 1) * 32 * PB, 1, PB, 16 * bi, 16 * bj,
+                           lane, -1.0, a[j][k]);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 }
 
 template <int R>
@@ -258,13 +255,23 @@ __global__ __launch_bounds__(256) void big_pivot_init_kernel(BigSpdBatch b) {
 // 16 w.. of the block for every row, so each Z_j stays in its registers: a 16x16 MFMA result in
 // the C layout (element (lk + 4 r, li) in acc[r]) is the B operand of the next product's k-steps
 // (k-step r reads B[4 r + lk][li]).  Row block i of Lg (L_i0 .. L_i,i-1, M_i) is staged in LDS.
-template <int R>
-__device__ __forceinline__ void panel_block(const BigSpdBatch& b, int m, int k, int J, double* sm) {
-  constexpr int NB = 2 * R;
+// Loads: the first two stages' X values are issued as soon as the panel row is in (wait.rows()),
+// before the wait for the pivot, the next ones two stages ahead, and each stage's L row block is
+// fetched into registers under the previous stage's products -- about one memory round trip per
+// panel instead of two per stage (the standalone C5 panel of sweep 0: 25 -> 15 us).  Same
+// products in the same order.
+struct NoPanelWait {
+  __device__ void rows() const {}
+  __device__ void pivot() const {}
+};
+template <int R, typename Wait = NoPanelWait>
+__device__ __forceinline__ void panel_block(const BigSpdBatch& b, int m, int k, int J, double* sm,
+                                            Wait wait = Wait()) {
+  constexpr int NB = 2 * R, W = BW * R;
   const int p = b.p[m], T = b.T[m];
   const int P0 = R * k;  // first 64-tile of the swept block
   if (P0 >= T || J >= T) return;
-  const int nb = min(BW * R, p - BW * P0) / 32;
+  const int nb = min(W, p - BW * P0) / 32;
   const int r0 = BW * P0, c0 = BW * J, wJ = bw(p, J);
   const bool own = J >= P0 && J < P0 + R;
   const double* X = b.X[m];
@@ -275,31 +282,63 @@ __device__ __forceinline__ void panel_block(const BigSpdBatch& b, int m, int k, 
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int li = lane & 15, lk = lane >> 4;
   const int col = c0 + 16 * wv + li;
+  wait.rows();
+  // X_i element e = t + 256 q: (r, c) = (e >> 6, e & 63) in row block P (J < P: coalesced along
+  // c), (e & 31, e >> 5) in column block P (J > P: X_{P,J}[r][c] = X[c0 + c][r0 + 32 i + r],
+  // coalesced along r); the identity in the swept columns
+  // (two stages in flight: a rolling pair of register sets, stage i + 2's loads issued once
+  // stage i is in LDS -- all four at once pushed the update kernel's tile loop into spills)
+  double xv[2][8];
+  auto xload = [&](double (&v)[8], int i) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = t + 256 * q;
+      double x = 0.0;
+      if (i < nb) {
+        if (own) {
+          x = (r0 + 32 * i + (e >> 6) == c0 + (e & 63)) ? 1.0 : 0.0;
+        } else if (J < P0) {
+          if ((e & 63) < wJ) x = X[(size_t)(r0 + 32 * i + (e >> 6)) * p + c0 + (e & 63)];
+        } else {
+          if ((e >> 5) < wJ) x = X[(size_t)(c0 + (e >> 5)) * p + r0 + 32 * i + (e & 31)];
+        }
+      }
+      v[q] = x;
+    }
+  };
+  xload(xv[0], 0);
+  xload(xv[1], 1);
+  wait.pivot();
+  // row block i of L: element e = t + 256 q, q < 4 (i + 1): block q >> 2, row (e >> 5) & 31, column e & 31
+  double lv[4 * NB];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = t + 256 * q;
+    lv[q] = Lg[(size_t)((e >> 5) & 31) * W + (e & 31)];
+  }
   d4 z[NB][2];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     if (i >= nb) break;
     if (i) __syncthreads();  // the previous stage's LDS reads are done
-    if (own) {
-      for (int e = t; e < 2048; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        sX[r * 65 + c] = (r0 + 32 * i + r == c0 + c) ? 1.0 : 0.0;
-      }
-    } else if (J < P0) {
-      for (int e = t; e < 2048; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        sX[r * 65 + c] = c < wJ ? X[(size_t)(r0 + 32 * i + r) * p + c0 + c] : 0.0;
-      }
-    } else {  // X_{P,J}[r][c] = X[c0 + c][r0 + 32 i + r]: coalesced along r
-      for (int e = t; e < 2048; e += 256) {
-        const int r = e & 31, c = e >> 5;
-        sX[r * 65 + c] = c < wJ ? X[(size_t)(c0 + c) * p + r0 + 32 * i + r] : 0.0;
-      }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = t + 256 * q;
+      if (own || J < P0) sX[(e >> 6) * 65 + (e & 63)] = xv[i & 1][q];
+      else sX[(e & 31) * 65 + (e >> 5)] = xv[i & 1][q];
     }
-    for (int e = t; e < 1024 * (i + 1); e += 256) {
-      const int q = e >> 10, r = (e >> 5) & 31, c = e & 31;
-      sL[q * 32 * PB + r * PB + c] = Lg[(size_t)(32 * i + r) * (BW * R) + 32 * q + c];
+    if (i + 2 < nb) xload(xv[i & 1], i + 2);
+#pragma unroll
+    for (int q = 0; q < 4 * (i + 1); ++q) {
+      const int e = t + 256 * q;
+      sL[(e >> 10) * 32 * PB + ((e >> 5) & 31) * PB + (e & 31)] = lv[q];
     }
+    if (i + 1 < nb)  // the next stage's row block, in flight under this stage's products
+#pragma unroll
+      for (int q = 0; q < 4 * (i + 2) && q < 4 * NB; ++q) {
+        const int e = t + 256 * q;
+        lv[q] = Lg[(size_t)(32 * (i + 1) + ((e >> 5) & 31)) * W + 32 * (e >> 10) + (e & 31)];
+      }
     __syncthreads();
     d4 acc[2];
 #pragma unroll
@@ -342,16 +381,23 @@ __global__ __launch_bounds__(256) void big_panel_kernel(BigSpdBatch b, int k) {
   panel_block<R>(b, blockIdx.y, k, blockIdx.x, sm);
 }
 
-// The next sweep's panel, fused into the update launch of sweep k (its last workgroups): it
-// waits for L^{-1} of pivot k + 1 (the pivot workgroup) and for the tiles of the next panel row
-// (counted by their workgroups), then fills zbuf(k + 1).  It waits only on workgroups dispatched
-// before it, none of which waits on it: no deadlock whatever the residency.
+// The next sweep's panel, fused into the update launch of sweep k: it waits for the tiles of the
+// next panel row (counted by their workgroups), issues its X loads, then waits for L^{-1} of pivot
+// k + 1 (the pivot workgroup), then fills zbuf(k + 1).
+struct PanelWait {
+  const unsigned int* fl;
+  int* status;
+  unsigned rows_target, pivot_target;
+  __device__ void rows() const { acquire_wait(fl + 2, rows_target, status); }
+  __device__ void pivot() const { acquire_wait(fl + 1, pivot_target, status); }
+};
+// Issue priority over the CU's other workgroup (a tile's product loop): the panel is a chain of
+// dependent MFMAs and LDS round trips on the sweep's critical path.
 template <int R>
-__device__ void fused_panel(const BigSpdBatch& b, int m, int k, int pj, unsigned int row_tiles, double* sm) {
-  const unsigned int* fl = b.flag[m];
-  acquire_wait(fl + 1, (unsigned)(k + 1), b.status[m]);
-  acquire_wait(fl + 2, (unsigned)(k + 1) * row_tiles, b.status[m]);
-  panel_block<R>(b, m, k + 1, pj, sm);
+__device__ __forceinline__ void fused_panel(const BigSpdBatch& b, int m, int k, int pj, unsigned int row_tiles, double* sm) {
+  __builtin_amdgcn_s_setprio(2);
+  panel_block<R>(b, m, k + 1, pj, sm, PanelWait{b.flag[m], b.status[m], (unsigned)(k + 1) * row_tiles, (unsigned)(k + 1)});
+  __builtin_amdgcn_s_setprio(0);
 }
 
 __device__ __forceinline__ void tile_of(int lin, int& I, int& J) {
@@ -656,6 +702,38 @@ constexpr int WT = 128;
 constexpr int WIDE_LDS = 2 * 2 * huge::KS * huge::S;  // the product loop's two staging buffers
 static_assert(WIDE_LDS >= PIVOT_LDS, "the pivot reuses the staging LDS");
 
+// position pos of sweep k's tile list of a factor with T2 128-tiles per dimension, with a next
+// pivot Q = k + 1: the T2 - 1 tiles the next panel reads first -- row Q left of the diagonal,
+// then column Q below it (round 0 of the factor's first XCD slot run: the panel's wait for its
+// row ends after one tile time instead of the last round) -- then every other lower tile in
+// row-major order; (Q, Q) is the pivot workgroup's, not listed.
+__device__ __forceinline__ void wide_tile_at(int pos, int T2, int Q, bool has_next, int& I, int& J) {
+  if (!has_next) {
+    tile_of(pos, I, J);
+    return;
+  }
+  if (pos < Q) {
+    I = Q;
+    J = pos;
+    return;
+  }
+  if (pos < T2 - 1) {
+    I = pos + 1;
+    J = Q;
+    return;
+  }
+  const int r = pos - (T2 - 1);
+  int i, j;
+  tile_of(r, i, j);
+  if (r < Q * (Q + 1) / 2) {  // rows above Q: row-major as they are
+    I = i;
+    J = j;
+    return;
+  }
+  I = i + 1;  // rows below Q hold I tiles each once column Q is taken out
+  J = j < Q ? j : j + 1;
+}
+
 __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int k, int skip_pivot, int gx,
                                                           int per_xcd, int nx, int first) {
   using namespace huge;
@@ -733,6 +811,10 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     const int Q = k + 1, qlin = Q * (Q + 1) / 2 + Q;
     int lin = wi % gx;
     if (lin >= nt - (has_next ? 1 : 0)) return false;
+    if (has_next && !skip_pivot) {  // the next panel row's tiles first (wide_tile_at)
+      wide_tile_at(lin, T2, Q, true, ti, tj);
+      return true;
+    }
     if (has_next && lin >= qlin) ++lin;  // (k+1, k+1) belongs to the pivot workgroup
     tile_of(lin, ti, tj);
     return true;
