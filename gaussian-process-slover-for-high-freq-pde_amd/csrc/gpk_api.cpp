@@ -1169,7 +1169,7 @@ static int reset_handoffs(gpk_handle* h) {
     if (h->PB2[a]) HIPCHK(hipMemsetD32Async(h->PB2[a], CHAIN_SENTINEL32, 4 * chain_half((int)P, h->chain_multi), h->s));
     if (h->cepoch[a]) HIPCHK(hipMemsetAsync(h->cepoch[a], 0, 4 * sizeof(unsigned int), h->s));
     HIPCHK(hipMemsetAsync(h->cflags[a], 0, nflags * sizeof(unsigned int), h->s));
-    HIPCHK(hipMemsetAsync(h->aflag[a], 0, 4 * sizeof(unsigned int), h->s));
+    HIPCHK(hipMemsetAsync(h->aflag[a], 0, (4 + P / 32) * sizeof(unsigned int), h->s));
   }
   HIPCHK(hipStreamSynchronize(h->s));
   return GPK_OK;
@@ -1496,7 +1496,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     A_(h->ldet[a], P / 32);
     A_(h->Kc[a], (size_t)P * P);
     A_(h->pst[a], 2);
-    A_(h->aflag[a], 4);
+    A_(h->aflag[a], 4 + P / 32);  // + the 128-wide update's per-sweep panel tickets
     if (h->bigspd) A_(h->Zp[a], (size_t)2 * 128 * P);
     A_(h->cflags[a], (size_t)(P / 32) * (P / 32 + (P1 + P2) / 32) + 2 * (P / 32) + 1);
     A_(h->cgran[a], (size_t)(P / 32) * 2048);
@@ -2559,6 +2559,80 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
       const double P = a == 0 ? L.p1 : L.p2;
       bytes += P * P * (4.0 + 8.0 + (h->Kc[a] ? 8.0 : 0.0) + (deriv ? 8.0 : 0.0));
     }
+  } else if ((nm == "write_stream" || nm == "write_stream_after_copy") && L.dim == 2) {
+    // a pure write stream of the gather's bytes (hipMemsetD32 of K, Kc, D of both factors),
+    // back to back or right after an HBM-bound copy of other buffers: whether the gather's
+    // in-step rate is the write-heavy HBM rate once the memory-side cache holds other lines
+    const bool after = nm == "write_stream_after_copy";
+    const size_t nb = (size_t)L.p1 * L.p2 * sizeof(double);
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    double tot = 0.0;
+    for (int it = 0; it <= iters; ++it) {
+      if (after)
+        for (int c = 0; c < 2; ++c) HIPCHK(hipMemcpyAsync(h->S, h->R, nb, hipMemcpyDeviceToDevice, h->s));
+      HIPCHK(hipEventRecord(e0, h->s));
+      for (int a = 0; a < L.naxes; ++a) {
+        const size_t P = a == 0 ? L.p1 : L.p2;
+        for (double* q : {h->K[a], h->Kc[a], h->D[a]}) HIPCHK(hipMemsetD32Async(q, 0, 2 * P * P, h->s));
+      }
+      HIPCHK(hipEventRecord(e1, h->s));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      if (it > 0) tot += ms * 1000.0;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (int a = 0; a < L.naxes; ++a) {
+      const double P = a == 0 ? L.p1 : L.p2;
+      bytes += 24.0 * P * P;
+    }
+    *avg_us = tot / iters;
+    *alg_flops = 0.0;
+    *alg_bytes = bytes;
+    return read_status(h);
+  } else if ((nm == "gather_after_gemm" || nm == "gather_after_copy") && L.dim == 2) {
+    // the gather timed alone (events around it) right after a C5-size GEMM stage (gemm_B: an
+    // MFMA-bound launch writing 2 x 134 MB) or after an HBM-bound copy of the same bytes: which
+    // state makes the in-step gather run at half its back-to-back rate
+    if (h->cls[0].ncls <= 0) return fail(GPK_EINVAL, "gather: this handle does not use distance classes");
+    for (int a = 0; a < L.naxes; ++a) {
+      aa[a].cls = h->cls[a];
+      aa[a].Kc = h->Kc[a];
+    }
+    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s, true),
+                     "class_eval"));
+    const bool gemm = nm == "gather_after_gemm";
+    const size_t nb = (size_t)L.p1 * L.p2 * sizeof(double);
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    double tot = 0.0;
+    for (int it = 0; it <= iters; ++it) {
+      if (gemm)
+        HIPCHK(launch_gemm_auto(h->hdescs.data() + h->st[3].off, h->st[3].n, h->sc, h->s, h->st[3].variant));
+      else
+        for (int c = 0; c < 2; ++c) HIPCHK(hipMemcpyAsync(h->S, h->R, nb, hipMemcpyDeviceToDevice, h->s));
+      HIPCHK(hipEventRecord(e0, h->s));
+      HIPCHK(launch_gather_only(aa, L.naxes, h->s));
+      HIPCHK(hipEventRecord(e1, h->s));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      if (it > 0) tot += ms * 1000.0;  // (the first is a warm-up)
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (int a = 0; a < L.naxes; ++a) {
+      const double P = a == 0 ? L.p1 : L.p2;
+      bytes += P * P * (4.0 + 8.0 + (h->Kc[a] ? 8.0 : 0.0) + (deriv ? 8.0 : 0.0));
+    }
+    *avg_us = tot / iters;
+    *alg_flops = 0.0;
+    *alg_bytes = bytes;
+    return read_status(h);
   } else if (nm == "class_eval") {
     // the class-value launch (every field at every class distance + the step constants): it
     // reads the U class distances and writes K and D values per class (24 B per class and axis)

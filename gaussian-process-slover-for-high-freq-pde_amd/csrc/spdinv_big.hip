@@ -245,6 +245,8 @@ __global__ __launch_bounds__(256) void big_pivot_init_kernel(BigSpdBatch b) {
     b.flag[m][1] = 0u;
     b.flag[m][2] = 0u;
   }
+  // the 128-wide update's per-sweep panel-block tickets (wide_update_kernel), one per sweep
+  for (int i = threadIdx.x; i < b.p[m] / 32; i += 256) b.flag[m][4 + i] = 0u;
 }
 
 // ---- the panel: Z_{:,J} = L^{-1} X_{P,J} by forward substitution over 32-row blocks ---------
@@ -751,19 +753,27 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   const int L = blockIdx.x;
   const bool probe = k == BIG_PROBE_SWEEP && threadIdx.x == 0;  // (trace build only)
   if (probe && L == 0) TR_LO(SLOT_BIG_START);
-  if (L >= 8 * nx + 8) {  // the next sweep's panel (fused_panel)
-    const int tmax = max(b.T[0], b.nmat > 1 ? b.T[1] : 0);
-    const int pi = L - 8 * nx - 8;
-    const int m = pi / tmax;
-    const int pj = pi % tmax;  // 64 columns per panel workgroup
-    if (m >= b.nmat) return;
+  if (L >= 8 * nx + 8) {  // the next sweep's panel (fused_panel), factors interleaved
+    const int m = (L - 8 * nx - 8) % b.nmat;
     const int T2 = (b.p[m] + WT - 1) / WT;
-    if (k + 1 >= T2 || skip_pivot || pj >= b.T[m]) return;
-    // T2 - 1 panel-row tiles per sweep, counted in quarter tiles (a whole tile adds 4)
-    if (probe && m == 0) TR_LO(SLOT_BIG_PANEL_WAIT);
-    fused_panel<2>(b, m, k, pj, 4u * (unsigned)(T2 - 1), sm);
-    if (probe && m == 0) TR_HI(SLOT_BIG_PANEL);
-    return;
+    if (k + 1 >= T2 || skip_pivot) return;
+    // Column blocks are claimed from a per-sweep ticket counter (zeroed with the pivot of block 0)
+    // instead of one per workgroup: the first panel workgroups find free slots at once (on the
+    // pivot workgroups' CUs, which the tile workgroups' second pass leaves with one free slot)
+    // and, once the pivot is in, keep taking blocks until the rest get CU slots as tile
+    // workgroups exit -- no block waits for a late workgroup.
+    __shared__ int s_tk;
+    unsigned int* ctr = b.flag[m] + 4 + k;
+    for (;;) {
+      if (threadIdx.x == 0) s_tk = (int)atomicAdd(ctr, 1u);
+      __syncthreads();
+      const int pj = s_tk;  // (read by every thread before fused_panel's first barrier)
+      if (pj >= b.T[m]) return;
+      // T2 - 1 panel-row tiles per sweep, counted in quarter tiles (a whole tile adds 4)
+      if (probe && m == 0) TR_LO(SLOT_BIG_PANEL_WAIT);
+      fused_panel<2>(b, m, k, pj, 4u * (unsigned)(T2 - 1), sm);
+      if (probe && m == 0) TR_HI(SLOT_BIG_PANEL);
+    }
   }
   const bool pivot = L >= first && L < first + 8;
   if (pivot && L - first >= b.nmat) return;

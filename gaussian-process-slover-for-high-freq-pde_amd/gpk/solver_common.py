@@ -153,20 +153,66 @@ class SolverBase(object):
     def _err(self, params):
         raise NotImplementedError
 
-    def train(self, nepoch, seed=0, verbose=True):
-        """train() (model_GP_solver_2d.py:235-352): same records, same early-stopping rule."""
+    # -- checkpoint / resume (the reference only pickles the final params,
+    # code/utils.py:580-597) ---------------------------------------------------------------
+    def save_checkpoint(self, path, loop=None):
+        """The training state as one NumPy .npz (plain arrays, no pickle): the flat params, the
+        Adam count / mu / nu (the device's optimizer state) and, from train(), the loop position
+        (epochs done, min error, error-increase count) and every record list."""
+        count, mu, nu = self.dev.get_opt_state()
+        arrs = {"params": self.dev.get_flat(), "count": np.int64(count), "mu": mu, "nu": nu}
+        if loop is not None:
+            done, min_err, inc, log = loop
+            arrs.update(done=np.int64(done), min_err=np.float64(min_err), inc=np.int64(inc))
+            for k, v in log.items():
+                arrs["log_" + k] = np.asarray(v)
+        np.savez(path, **arrs)
+
+    def load_checkpoint(self, path):
+        """Restore a save_checkpoint() file onto the device; returns the train-loop state or None."""
+        with np.load(path, allow_pickle=False) as z:
+            self.dev.set_flat(z["params"])
+            self._version += 1
+            self.dev.set_opt_state(int(z["count"]), z["mu"], z["nu"])
+            if "done" not in z:
+                return None
+            # (per-record arrays stay arrays, scalars Python numbers: as train() appends them)
+            log = {k[4:]: [x.copy() if x.ndim else x.item() for x in z[k]] for k in z.files if k.startswith("log_")}
+            return int(z["done"]), float(z["min_err"]), int(z["inc"]), log
+
+    def train(self, nepoch, seed=0, verbose=True, checkpoint=None, resume=None, stop_at=None, perf_log=None):
+        """train() (model_GP_solver_2d.py:235-352): same records, same early-stopping rule.
+
+        Beyond the reference: `checkpoint` (path) saves the training state after every record
+        epoch (save_checkpoint), `resume` (path) continues from such a file -- the same records
+        and the same device state as the uninterrupted run -- and `stop_at` ends the loop after
+        the first record at or past that many epochs (a time-boxed job, resumed later).
+        `perf_log` (path) appends one JSON line per record: epoch, loss, error, criterion, and
+        the device steps and wall time of the batch before it."""
+        import json
+        import time
         early_stopping = {"flag": False, "epoch": self.trick_paras["nepoch"]}
         params = self.init_params()
         self._sync(params)
         self.reset_optimizer()
         log = {"loss_list": [], "err_list": [], "epoch_list": []}
         min_err, threshold, error_increase_count = 2.0, 1e-3, 0
-        rec = record_epochs(nepoch)
-        bar = _tqdm.tqdm(total=nepoch, disable=not verbose) if _tqdm is not None else None
         done = 0
+        if resume is not None:
+            st = self.load_checkpoint(resume)
+            if st is None:
+                raise ValueError("resume: %s holds no train-loop state" % resume)
+            done, min_err, error_increase_count, log = st
+        rec = record_epochs(nepoch)
+        bar = _tqdm.tqdm(total=nepoch, initial=done, disable=not verbose) if _tqdm is not None else None
         for i in rec + [nepoch]:
+            if i < nepoch and i + 1 <= done:
+                continue  # (recorded before the checkpoint this run resumed from)
             n = (i + 1 - done) if i < nepoch else (nepoch - done)
+            t0 = time.perf_counter()
             losses = self.steps(n)
+            self.dev.sync()
+            dt = time.perf_counter() - t0
             done += n
             if bar is not None:
                 bar.update(n)
@@ -189,6 +235,14 @@ class SolverBase(object):
             criterion = self.compute_early_stopping(params)
             if verbose:
                 print("criterion = %g" % criterion)
+            if perf_log is not None:
+                with open(perf_log, "a") as f:
+                    f.write(json.dumps({"epoch": i, "loss": loss, "err": float(err), "criterion": float(criterion),
+                                        "steps": int(n), "seconds": dt, "steps_per_s": n / dt if dt > 0 else None}) + "\n")
+            if checkpoint is not None:
+                self.save_checkpoint(checkpoint, (done, min_err, error_increase_count, log))
+            if stop_at is not None and done >= stop_at:
+                break
             if self.early_stop_enabled and self.trick_paras.get("tol", -1) > 0 and criterion < self.trick_paras["tol"]:
                 if verbose:
                     print("early stop at epoch %d" % i)

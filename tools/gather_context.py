@@ -1,6 +1,7 @@
-"""The C5 K-assembly launch (gather_wide_kernel) timed in two contexts on one handle: back to back
-(gpk_bench_kernel "gather", HIP events) and inside whole steps; run under rocprofv3 --kernel-trace
-to get every dispatch's duration in order.
+"""The C5 K-assembly launch (gather_wide_kernel) timed in several contexts on one handle: back to
+back (gpk_bench_kernel "gather", HIP events), right after a C5 GEMM stage (gather_after_gemm) or
+after an HBM-bound copy of the same bytes (gather_after_copy), and inside whole steps; run under
+rocprofv3 --kernel-trace to get every dispatch's duration in order.
 
     rocprofv3 --kernel-trace -f csv -d DIR -- python3 tools/gather_context.py
 """
@@ -18,5 +19,8 @@ try:
     s.sync()
     us, fl, by = s.bench_kernel("gather", 5)
     print(f"bench gather again (events): {us:.1f} us  {by / us / 1e3:.0f} GB/s", flush=True)
+    for ctx in ("gather_after_gemm", "gather_after_copy", "gather", "write_stream", "write_stream_after_copy"):
+        us, fl, by = s.bench_kernel(ctx, 5)
+        print(f"{ctx:18s} (events around the gather alone): {us:.1f} us  {by / us / 1e3:.0f} GB/s", flush=True)
 finally:
     s.close()

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-3 measurement session: GPU suite (parity log), smoke, the driver-shape bench line, and
+# Round-4 measurement session: GPU suite (parity log), smoke, the driver-shape bench line, and
 # rocprofv3 traces + PMC passes (HBM FETCH/WRITE, fp64 MFMA) for C4 (bench), C5 and C2.
 set -o pipefail
-OUT=${OUT:-gpurun_out/r3p}
+OUT=${OUT:-gpurun_out/r4p}
 mkdir -p $OUT
 export TMPDIR=/tmp
 export GPK_PARITY_LOG=$OUT/parity.jsonl
