@@ -263,7 +263,12 @@ __global__ __launch_bounds__(256) void gather_kernel(AssembleBatch b) {
 // D pairs out, whole 1-KiB row segments per wave instruction), all 8 of a lane's class-id loads
 // issued before its gathers and stores (memory-level parallelism), nontemporal stores.  C5 (two
 // 4096^2 factors): 940 MB per launch (K, Kc, D written, the ids read).
-constexpr int GW_ROWS = 8, GW_COLS = 512;
+// GW_H row pairs of 4 per workgroup (one row per wave and pair): 16 rows x 512 columns, every
+// class id of the block loaded in one batch (16 int2 per thread) before the dependent class-value
+// loads.  In a step the ids come from HBM -- the memory-side cache holds the previous kernels'
+// lines, not the ids -- and with 8 rows per workgroup the launch ran at half its back-to-back
+// rate (a pure write stream of the same bytes does not slow down: profiles/r4_gather_context.txt)
+constexpr int GW_H = 4, GW_ROWS = 4 * GW_H, GW_COLS = 512;
 constexpr int GW_WIDE_MIN_TILES = 1024;  // 32x32 tiles: P >= 1024
 template <int DERIV>
 __global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b) {
@@ -274,10 +279,10 @@ __global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b) {
   const int r0 = blockIdx.y * GW_ROWS, c0 = blockIdx.x * GW_COLS;
   if (r0 >= p || c0 >= p) return;  // (the shorter axis)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  int2 id[2][4];
-  int row[2], col[4];
+  int2 id[GW_H][4];
+  int row[GW_H], col[4];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < GW_H; ++h) {
     row[h] = r0 + w + 4 * h;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -286,17 +291,17 @@ __global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b) {
                               : make_int2(-1, -1);
     }
   }
-  double xi[2] = {0.0, 0.0};
+  double xi[GW_H] = {};
   double2 xj[4];
   if (DERIV == 1) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) xi[h] = A.x[min(row[h], A.n - 1)];
+    for (int h = 0; h < GW_H; ++h) xi[h] = A.x[min(row[h], A.n - 1)];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       xj[q] = make_double2(A.x[min(col[q], A.n - 1)], A.x[min(col[q] + 1, A.n - 1)]);
   }
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < GW_H; ++h)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (col[q] >= p) continue;
