@@ -270,80 +270,118 @@ __global__ __launch_bounds__(256) void gather_kernel(AssembleBatch b) {
 // rate (a pure write stream of the same bytes does not slow down: profiles/r4_gather_context.txt)
 constexpr int GW_H = 4, GW_ROWS = 4 * GW_H, GW_COLS = 512;
 constexpr int GW_WIDE_MIN_TILES = 1024;  // 32x32 tiles: P >= 1024
+// Persistent: GW_WGS workgroups walk the blocks (axis, row block, column block) with a stride of
+// the grid, and each issues the NEXT block's class ids before it gathers and stores the current
+// one, so the store stream does not stall on the id loads' HBM latency.
+constexpr int GW_WGS = 2048;
 template <int DERIV>
-__global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b) {
-  const int axis = blockIdx.z;
-  const AssembleArgs& A = b.ax[axis];
-  const ClassArgs& C = A.cls;
-  const int p = A.p;
-  const int r0 = blockIdx.y * GW_ROWS, c0 = blockIdx.x * GW_COLS;
-  if (r0 >= p || c0 >= p) return;  // (the shorter axis)
+__global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b, int nbx, int nby, int nblk) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  int2 id[GW_H][4];
-  int row[GW_H], col[4];
+  // block -> (axis, r0, c0); false past the shorter axis
+  auto where = [&](int blk, int& axis, int& r0, int& c0) -> bool {
+    axis = blk / (nbx * nby);
+    const int rem = blk - axis * nbx * nby;
+    r0 = (rem / nbx) * GW_ROWS;
+    c0 = (rem % nbx) * GW_COLS;
+    const int p = axis ? b.ax[1].p : b.ax[0].p;
+    return r0 < p && c0 < p;
+  };
+  auto load_ids = [&](int2 (&id)[GW_H][4], int axis, int r0, int c0) {
+    const int* cid = axis ? b.ax[1].cls.cid : b.ax[0].cls.cid;
+    const int p = axis ? b.ax[1].p : b.ax[0].p;
 #pragma unroll
-  for (int h = 0; h < GW_H; ++h) {
-    row[h] = r0 + w + 4 * h;
+    for (int h = 0; h < GW_H; ++h)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      col[q] = c0 + 128 * q + 2 * lane;
-      id[h][q] = (col[q] < p) ? *reinterpret_cast<const int2*>(C.cid + (size_t)row[h] * p + col[q])
-                              : make_int2(-1, -1);
-    }
-  }
-  double xi[GW_H] = {};
-  double2 xj[4];
-  if (DERIV == 1) {
-#pragma unroll
-    for (int h = 0; h < GW_H; ++h) xi[h] = A.x[min(row[h], A.n - 1)];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      xj[q] = make_double2(A.x[min(col[q], A.n - 1)], A.x[min(col[q] + 1, A.n - 1)]);
-  }
-#pragma unroll
-  for (int h = 0; h < GW_H; ++h)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (col[q] >= p) continue;
-      const int i = row[h];
-      double kv[2], dv[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int u = e == 0 ? id[h][q].x : id[h][q].y, j = col[q] + e;
-        if (u >= 0) {
-          kv[e] = C.kval[u];
-          if (i == j) kv[e] += A.jitter;
-          dv[e] = C.dval[u];
-          if (DERIV == 1) {
-            const double xjj = e == 0 ? xj[q].x : xj[q].y;
-            if (!(xi[h] - xjj >= 0.0)) dv[e] = -dv[e];  // JAX abs'(0) = +1
-          }
-        } else {
-          kv[e] = (i == j) ? 1.0 : 0.0;
-          dv[e] = 0.0;
-        }
+      for (int q = 0; q < 4; ++q) {
+        const int col = c0 + 128 * q + 2 * lane;
+        id[h][q] = (col < p) ? *reinterpret_cast<const int2*>(cid + (size_t)(r0 + w + 4 * h) * p + col)
+                             : make_int2(-1, -1);
       }
-      // nontemporal stores: 3.4 -> 7.0 TB/s at C5 size (tools/probes/gather_probe.hip; write-
-      // allocating stores held the launch at 3.4-3.7 TB/s whatever the layout); the next readers
-      // (the inverse, the GEMMs) run on other XCDs and read from memory anyway
-      // (one 16-B store per array and lane: per-element stores interleaved across the arrays
-      // were not merged and ran at 1.9 TB/s)
-      typedef double d2v __attribute__((ext_vector_type(2)));
-      const size_t o = (size_t)i * p + col[q];
-      const d2v k2 = {kv[0], kv[1]}, d2 = {dv[0], dv[1]};
-      __builtin_nontemporal_store(k2, reinterpret_cast<d2v*>(A.K + o));
-      if (A.Kc) __builtin_nontemporal_store(k2, reinterpret_cast<d2v*>(A.Kc + o));
-      if (DERIV) __builtin_nontemporal_store(d2, reinterpret_cast<d2v*>(A.D + o));
+  };
+  auto process = [&](const int2 (&id)[GW_H][4], int axis, int r0, int c0) {
+    const AssembleArgs& A = axis ? b.ax[1] : b.ax[0];
+    const double* kval = A.cls.kval;
+    const double* dval = A.cls.dval;
+    const int p = A.p;
+    int row[GW_H], col[4];
+#pragma unroll
+    for (int h = 0; h < GW_H; ++h) row[h] = r0 + w + 4 * h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) col[q] = c0 + 128 * q + 2 * lane;
+    double xi[GW_H] = {};
+    double2 xj[4];
+    if (DERIV == 1) {
+#pragma unroll
+      for (int h = 0; h < GW_H; ++h) xi[h] = A.x[min(row[h], A.n - 1)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        xj[q] = make_double2(A.x[min(col[q], A.n - 1)], A.x[min(col[q] + 1, A.n - 1)]);
     }
+#pragma unroll
+    for (int h = 0; h < GW_H; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (col[q] >= p) continue;
+        const int i = row[h];
+        double kv[2], dv[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int u = e == 0 ? id[h][q].x : id[h][q].y, j = col[q] + e;
+          if (u >= 0) {
+            kv[e] = kval[u];
+            if (i == j) kv[e] += A.jitter;
+            dv[e] = dval[u];
+            if (DERIV == 1) {
+              const double xjj = e == 0 ? xj[q].x : xj[q].y;
+              if (!(xi[h] - xjj >= 0.0)) dv[e] = -dv[e];  // JAX abs'(0) = +1
+            }
+          } else {
+            kv[e] = (i == j) ? 1.0 : 0.0;
+            dv[e] = 0.0;
+          }
+        }
+        // nontemporal stores: 3.4 -> 7.0 TB/s at C5 size (tools/probes/gather_probe.hip; write-
+        // allocating stores held the launch at 3.4-3.7 TB/s whatever the layout); the next readers
+        // (the inverse, the GEMMs) run on other XCDs and read from memory anyway
+        // (one 16-B store per array and lane: per-element stores interleaved across the arrays
+        // were not merged and ran at 1.9 TB/s)
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const size_t o = (size_t)i * p + col[q];
+        const d2v k2 = {kv[0], kv[1]}, d2 = {dv[0], dv[1]};
+        __builtin_nontemporal_store(k2, reinterpret_cast<d2v*>(A.K + o));
+        if (A.Kc) __builtin_nontemporal_store(k2, reinterpret_cast<d2v*>(A.Kc + o));
+        if (DERIV) __builtin_nontemporal_store(d2, reinterpret_cast<d2v*>(A.D + o));
+      }
+  };
+  int2 ida[GW_H][4], idb[GW_H][4];
+  int blk = blockIdx.x, ax, r0, c0;
+  while (blk < nblk && !where(blk, ax, r0, c0)) blk += gridDim.x;
+  if (blk >= nblk) return;
+  load_ids(ida, ax, r0, c0);
+  for (;;) {  // two blocks per trip: the id arrays alternate (registers, not indexed)
+    int nb = blk + gridDim.x, ax2 = 0, r2 = 0, c2 = 0;
+    while (nb < nblk && !where(nb, ax2, r2, c2)) nb += gridDim.x;
+    if (nb < nblk) load_ids(idb, ax2, r2, c2);
+    process(ida, ax, r0, c0);
+    if (nb >= nblk) return;
+    blk = nb; ax = ax2; r0 = r2; c0 = c2;
+    nb = blk + gridDim.x;
+    while (nb < nblk && !where(nb, ax2, r2, c2)) nb += gridDim.x;
+    if (nb < nblk) load_ids(ida, ax2, r2, c2);
+    process(idb, ax, r0, c0);
+    if (nb >= nblk) return;
+    blk = nb; ax = ax2; r0 = r2; c0 = c2;
+  }
 }
 
 static void launch_gather_wide(const AssembleBatch& b, int naxes, int deriv, hipStream_t s) {
   int pmax = 0;
   for (int k = 0; k < naxes; ++k) pmax = std::max(pmax, b.ax[k].p);
-  dim3 g((pmax + GW_COLS - 1) / GW_COLS, (pmax + GW_ROWS - 1) / GW_ROWS, naxes);
-  if (deriv == 2) hipLaunchKernelGGL((gather_wide_kernel<2>), g, dim3(256), 0, s, b);
-  else if (deriv == 1) hipLaunchKernelGGL((gather_wide_kernel<1>), g, dim3(256), 0, s, b);
-  else hipLaunchKernelGGL((gather_wide_kernel<0>), g, dim3(256), 0, s, b);
+  const int nbx = (pmax + GW_COLS - 1) / GW_COLS, nby = (pmax + GW_ROWS - 1) / GW_ROWS, nblk = nbx * nby * naxes;
+  const dim3 g(std::min(nblk, GW_WGS));
+  if (deriv == 2) hipLaunchKernelGGL((gather_wide_kernel<2>), g, dim3(256), 0, s, b, nbx, nby, nblk);
+  else if (deriv == 1) hipLaunchKernelGGL((gather_wide_kernel<1>), g, dim3(256), 0, s, b, nbx, nby, nblk);
+  else hipLaunchKernelGGL((gather_wide_kernel<0>), g, dim3(256), 0, s, b, nbx, nby, nblk);
 }
 
 template <bool MATERN, bool COS>

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4: the gather in its step contexts, libgpk.so vs libgpk_abgat.so (HEAD's gather), interleaved
+# round 4: the gather in its step contexts, libgpk.so vs libgpk_abgat.so, interleaved
 set -o pipefail
 mkdir -p gpurun_out/r4
 export TMPDIR=/tmp
