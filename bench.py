@@ -43,7 +43,7 @@ KERNEL_LAUNCHES = {"spd_chain": 1, "sweep": None, "gemm_B": 3, "pgrad": 1, "asse
 
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench (tools/gpu_round.sh), summarised by
 # tools/pmc_summary.py: HBM-side bytes per launch (2*FETCH + WRITE, MI355X_MICROARCH.md §HBM)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r3_pmc_c4.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r4_pmc_c4.json")
 if not os.path.exists(PMC_SUMMARY):
     PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2_pmc_c4.json")
 PMC_KERNEL = {"spd_chain": "gpk::chain_kernel<2, true>", "sweep": "gpk::sweep_kernel",
