@@ -11,6 +11,7 @@
 // see "row-sharded multi-GPU step" below.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <atomic>
@@ -127,6 +128,7 @@ struct gpk_handle {
   int ttg = 0, tngpa = 0;
   std::vector<GemmDesc> hdescs;  // per-stage GEMM descriptors (kernel arguments)
   Stage st[kGemmStages];
+  rocblas_handle rb = nullptr;   // the plain products of 128x128-tile stages (lib_plain)
   double *Kc[2] = {}, *pst[2] = {};  // kept K (refinement residuals), pivot stats (gate)
   unsigned int* aflag[2] = {};        // assembly -> pivot-0 hand-off counters (small path) /
                                       // update -> pivot hand-off counters (large path)
@@ -419,6 +421,75 @@ static void gemv_operand(const gpk_handle* h, GemvDesc& g) {
 
 static int enqueue_step_shard(gpk_handle* h, int apply);
 
+// A plain product -- one product C = alpha op(A) op(B) [+ beta C0], host-constant alpha and
+// beta, no refinement gate, epilogue, partial sums or side output -- of a stage that runs on
+// the 128x128-tile kernel is a plain library GEMM: rocBLAS (deterministic: atomics off by
+// default), which outruns gemm_huge_kernel on these shapes (tools/dgemm_library.py, 4096^3:
+// 67.8 / 74.1 / 73.3 TF/s NN / TN / NT against ~64).  The fused stages and the v-scaled products
+// (alpha * v, v on the device: rocBLAS's device pointer mode returned an internal error here)
+// stay on our kernels.
+static bool lib_plain(const GemmDesc& g) {
+  return g.epi == EPI_STORE && !g.gate && !g.Y && !g.red && !g.red2 && g.K2 == 0 && !g.vscale &&
+         !g.vscale2;
+}
+static int lib_gemm(gpk_handle* h, const GemmDesc& g) {
+  const rocblas_operation oa = g.ta ? rocblas_operation_transpose : rocblas_operation_none;
+  const rocblas_operation ob = g.tb ? rocblas_operation_transpose : rocblas_operation_none;
+  const double alpha = g.alpha, beta = g.C0 ? g.beta : 0.0;
+  const double* c = g.C0 ? g.C0 : g.C;
+  const int ldc = g.C0 ? g.ldc0 : g.ldc;
+  // row-major C = op(A) op(B) is column-major C^T = op(B)^T op(A)^T: B first, M and N swapped
+  const rocblas_status st = rocblas_gemm_ex(
+      h->rb, ob, oa, g.N, g.M, g.K, &alpha, g.B, rocblas_datatype_f64_r, g.ldb, g.A,
+      rocblas_datatype_f64_r, g.lda, &beta, c, rocblas_datatype_f64_r, ldc, g.C, rocblas_datatype_f64_r,
+      g.ldc, rocblas_datatype_f64_r, rocblas_gemm_algo_standard, 0, 0);
+  if (st != rocblas_status_success)
+    return fail(GPK_EHIP, std::string("rocblas_gemm_ex: ") + rocblas_status_to_string(st));
+  return GPK_OK;
+}
+static int launch_stage(gpk_handle* h, int k) {
+  const GemmDesc* ds = h->hdescs.data() + h->st[k].off;
+  const int n = h->st[k].n;
+  if (!h->rb || h->st[k].variant != GEMM_HUGE)
+    return check_launch(launch_gemm_auto(ds, n, h->sc, h->s, h->st[k].variant), "gemm");
+  GemmDesc rest[GEMM_MAX_BATCH];
+  int nr = 0;
+  for (int i = 0; i < n; ++i) {
+    if (lib_plain(ds[i])) {
+      TRY(lib_gemm(h, ds[i]));
+    } else {
+      rest[nr++] = ds[i];
+    }
+  }
+  if (nr) return check_launch(launch_gemm_auto(rest, nr, h->sc, h->s, GEMM_HUGE), "gemm");
+  return GPK_OK;
+}
+// rocBLAS for the plain products of 128x128-tile stages (unsharded 2D handles; GPK_NO_LIB_GEMM
+// set in the environment keeps every product on gemm_huge_kernel).  The workspace is preset and
+// every library product runs once here, outside any capture: no allocation or code-object load
+// inside a step graph's capture.  (The warm calls write only stage outputs every step rewrites.)
+static int setup_lib_gemm(gpk_handle* h) {
+  if (std::getenv("GPK_NO_LIB_GEMM")) return GPK_OK;
+  std::vector<int> plain;
+  for (int k = 0; k < kGemmStages; ++k)
+    if (h->st[k].variant == GEMM_HUGE)
+      for (int i = h->st[k].off; i < h->st[k].off + h->st[k].n; ++i)
+        if (lib_plain(h->hdescs[i])) plain.push_back(i);
+  if (plain.empty()) return GPK_OK;
+  if (rocblas_create_handle(&h->rb) != rocblas_status_success) return fail(GPK_EHIP, "rocblas_create_handle");
+  if (rocblas_set_stream(h->rb, h->s) != rocblas_status_success ||
+      rocblas_set_pointer_mode(h->rb, rocblas_pointer_mode_host) != rocblas_status_success)
+    return fail(GPK_EHIP, "rocblas handle setup");
+  constexpr size_t kWs = size_t(64) << 20;
+  void* ws = nullptr;
+  HIPCHK(hipMalloc(&ws, kWs));
+  h->allocs.push_back(ws);
+  if (rocblas_set_workspace(h->rb, ws, kWs) != rocblas_status_success) return fail(GPK_EHIP, "rocblas_set_workspace");
+  for (int i : plain) TRY(lib_gemm(h, h->hdescs[i]));
+  HIPCHK(hipStreamSynchronize(h->s));
+  return GPK_OK;
+}
+
 static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
   if (h->shard) return enqueue_step_shard(h, apply);
   const Layout& L = h->L;
@@ -438,8 +509,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
   if (L.dim == 2) {
     for (int k = 0; k < kGemmStages; ++k) {
       if (h->st[k].n == 0 || (!refine && h->st[k].gated)) continue;
-      TRY(check_launch(launch_gemm_auto(h->hdescs.data() + h->st[k].off, h->st[k].n, h->sc, h->s,
-                                        h->st[k].variant), "gemm"));
+      TRY(launch_stage(h, k));
       stamp(kStageNames2D[3 + k]);
     }
     PGradArgs pa[2];
@@ -1611,6 +1681,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   }
   if (L.dim == 2 && (rc = build_descs(h)) != GPK_OK) return bail(rc);
   if (shard && (rc = build_shard(h)) != GPK_OK) return bail(rc);
+  if (L.dim == 2 && !shard && (rc = setup_lib_gemm(h)) != GPK_OK) return bail(rc);
   // (the 2D large-factor path has no refinement stages: its one graph is the fast one)
   h->fast_ok = !shard && !(h->bigspd && L.dim == 2) && !(p->flags & GPK_FLAG_NO_FAST_GRAPH);
   h->fast_mode = h->fast_ok && (p->flags & GPK_FLAG_FAST_FIRST);
@@ -1791,6 +1862,7 @@ int gpk_destroy(gpk_handle* h) {
   for (int k = 0; k <= kMaxStages; ++k)
     if (h->ev[k]) (void)hipEventDestroy(h->ev[k]);
   if (h->rep_host) (void)hipHostFree(h->rep_host);
+  if (h->rb) (void)rocblas_destroy_handle(h->rb);
   for (void* p : h->allocs) (void)hipFree(p);
   if (h->s) (void)hipStreamDestroy(h->s);
   delete h->comm;
