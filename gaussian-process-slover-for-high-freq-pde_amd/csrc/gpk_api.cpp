@@ -129,6 +129,7 @@ struct gpk_handle {
   std::vector<GemmDesc> hdescs;  // per-stage GEMM descriptors (kernel arguments)
   Stage st[kGemmStages];
   rocblas_handle rb = nullptr;   // the plain products of 128x128-tile stages (lib_plain)
+  bool gd_v = false;             // G_D stored without its v (a plain product), v in the contraction
   double *Kc[2] = {}, *pst[2] = {};  // kept K (refinement residuals), pivot stats (gate)
   unsigned int* aflag[2] = {};        // assembly -> pivot-0 hand-off counters (small path) /
                                       // update -> pivot hand-off counters (large path)
@@ -521,6 +522,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
       pa[a].kc = h->kc + a;
       pa[a].GK = h->GK[a];
       pa[a].GD = h->GD[a];
+      pa[a].gd_v = h->gd_v ? 1 : 0;
       pa[a].deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
       pa[a].cls = h->cls[a];
@@ -736,11 +738,14 @@ static int build_descs(gpk_handle* h) {
     d.push_back(mk(h->R, P2, 0, h->D[1], P2, 0, h->T2, P2, P1, P2, P2));
   }
   {
+    // large unsharded factors: G_D / v, a plain product (lib_plain: rocBLAS with a host alpha);
+    // the contraction multiplies its G_D weights by v (PGradArgs::gd_v)
+    h->gd_v = h->bigspd && !h->shard && !std::getenv("GPK_NO_LIB_GEMM");
     GemmDesc g = mk(h->R, P2, 0, h->A, P2, 1, h->GD[0], P1, P1, P1, P2);
-    g.alpha = beta; g.vscale = 1;
+    g.alpha = beta; g.vscale = h->gd_v ? 0 : 1;
     d.push_back(g);
     GemmDesc g2 = mk(h->R, P2, 1, h->Bt, P2, 0, h->GD[1], P2, P2, P2, P1);
-    g2.vscale = 1;
+    g2.vscale = h->gd_v ? 0 : 1;
     d.push_back(g2);
   }
   end(6);
@@ -2742,6 +2747,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
       pa[a] = PGradArgs{};
       pa[a].x = a == 0 ? h->x1 : h->x2; pa[a].n = a == 0 ? L.n1 : L.n2; pa[a].p = a == 0 ? L.p1 : L.p2;
       pa[a].kc = h->kc + a; pa[a].GK = h->GK[a]; pa[a].GD = h->GD[a]; pa[a].deriv = deriv;
+      pa[a].gd_v = h->gd_v ? 1 : 0;
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
       pa[a].cls = h->cls[a];
     }

@@ -367,6 +367,7 @@ struct PGradArgs {
   const double* x; int n; int p;
   const AxisConst* kc;
   const double* GK; const double* GD;     // 2D mode: materialised [p*p]
+  int gd_v;                               // 1: GD holds G_D / v (library products), v applied here
   const double* Kinv;                     // 1D mode
   const double* alpha; const double* beta; const double* R;  // 1D mode vectors
   double halfc;                           // 1D mode: 0.5*logdet flag
