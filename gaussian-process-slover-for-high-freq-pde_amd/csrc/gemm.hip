@@ -11,7 +11,7 @@
 // (A[i=l&15][k=l>>4], B[k=l>>4][j=l&15], C/D row=(l>>4)+4r, col=l&15).
 #include "gpk_internal.h"
 #include "gpk_trace.h"
-#include "gemm_huge_dev.h"
+#include "gemm_tile_dev.h"
 
 #include <algorithm>
 
@@ -586,25 +586,30 @@ __global__ __launch_bounds__(256) void gemm_big_kernel(GemmBatch batch, const St
 
 // ---------------------------------------------------------------------------------------
 // Largest-size variant (M, N >= ~2048, e.g. the 4096^2 advection grid): a 128x128 output tile
-// per 256-thread workgroup, each wave a 64x64 quadrant = 4x4 v_mfma_f64_16x16x4 blocks (every
-// LDS fragment feeds 4 MFMAs, 16 independent accumulation chains per wave); 16-deep K-steps
-// through double-buffered LDS ([k][m] / [k][n], rows 140 doubles apart: gemm_huge_dev.h), the next
-// step prefetched global -> registers with 16-B loads that read whole contiguous segments.
-// A dual product is folded into the same accumulators: its A2 operand is scaled by
-// alpha2 / alpha on the way into LDS, and the epilogue applies alpha once.  Tiles are dealt
-// XCD-major and walked in groups of 4 tile rows (A/B panel reuse in each XCD's L2).
-// 128x128 tiles measured 55.9 TF/s on 4096^3 NN vs 40.2 TF/s for the 64x64 kernel
-// (tools/probes/gemm128_probe.hip).
+// per 256-thread workgroup, each wave a 64x64 quadrant = 4x4 v_mfma_f64_16x16x4 blocks, the
+// software-pipelined product loop of gemm_tile_dev.h (no operand transposed on its way into LDS,
+// one barrier per 16-deep K-step between the two MFMA half steps, stores / loads / reads
+// interleaved with the MFMAs).  A dual product is folded into the same accumulators: its A2
+// operand is scaled by alpha2 / alpha on the way into LDS, and the epilogue applies alpha once.
+// Tiles are dealt XCD-major and walked in groups of 4 tile rows (A/B panel reuse in each XCD's
+// L2).  4096^3: 71.8 (NN) / 73.4 (NT) / 73.1 (TN) / 73.4 (TT) TF/s, against 65 TF/s for the
+// previous 16-deep-step loop and 66.8 / 73.2 / 73.2 for the library (tools/probes/
+// gemm_tile_probe.hip, profiles/r5_tile_probe1.txt).
 // ---------------------------------------------------------------------------------------
-// namespace huge: gemm_huge_dev.h
 
-// one instantiation per transpose signature of (product, dual product): the K-loops carry no
-// branches at all (a runtime transpose switch makes the compiler shuttle the accumulators
-// between AGPRs and VGPRs every K-step); the launcher splits a batch by signature.
-template <int TA, int TB, int TA2, int TB2>
-__global__ __launch_bounds__(256) void gemm_huge_kernel(GemmBatch batch, const StepScalars* __restrict__ sc,
-                                                        int per_xcd) {
-  using namespace huge;
+// one instantiation per transpose signature: the K-loop carries no branches at all (a runtime
+// transpose switch makes the compiler shuttle the accumulators between AGPRs and VGPRs every
+// K-step).  A dual product runs as two launches (launch_huge): the first stores
+// alpha op(A) op(B) [+ beta C0] into C, the second adds alpha2 op(A2) op(B2) to it (Cp) and runs
+// the epilogue -- one product loop per kernel keeps the loop's 224 live VGPRs (128 accumulator,
+// 64 fragment, 32 global-prefetch) spill-free, for one extra pass over C (at 4096^2 about 35 us
+// against the 4.4 ms of the two products).
+// waves_per_eu(2): 256 VGPRs per lane and two workgroups per CU (2 x 68 KB of LDS).
+template <int TA, int TB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void gemm_huge_kernel(GemmBatch batch, const StepScalars* __restrict__ sc, int per_xcd) {
+  using namespace tile;
+  constexpr int GROUP_M = 4;
   const GemmDesc& d = batch.d[blockIdx.y];
   const int tm = (d.M + TM - 1) / TM, tn = (d.N + TM - 1) / TM;
   const int o = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);  // XCD-major dealing
@@ -615,40 +620,53 @@ __global__ __launch_bounds__(256) void gemm_huge_kernel(GemmBatch batch, const S
   const int ti = first + in % gm, tj = in / gm;
   const int tile = ti * tn + tj;  // partial-sum slot (row-major tile index)
   const int i0 = ti * TM, j0 = tj * TM;
-  __shared__ double sA[2 * KS * S], sB[2 * KS * S];
+  __shared__ double lds[LDS_DOUBLES];
   __shared__ double sred[4], sred2[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  double alpha = d.alpha, alpha2 = d.alpha2;
-  if (d.vscale) alpha *= sc->v;
-  if (d.vscale2) alpha2 *= sc->v;
-  const double vv = d.Y ? sc->v : 0.0;
   d4 acc[4][4];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[x][y] = d4{0.0, 0.0, 0.0, 0.0};
-  product_t<TA, TB>(d.A, d.lda, d.B, d.ldb, d.K, d.M, d.N, i0, j0, 1.0, sA, sB, t, wr, wc, lane, acc);
-  if (d.K2)
-    product_t<TA2, TB2>(d.A2, d.lda2, d.B2, d.ldb2, d.K2, d.M, d.N, i0, j0, alpha2 / alpha, sA, sB, t,
-                        wr, wc, lane, acc);
+  product<TA, TB, false, 0>(d.A, d.lda, d.B, d.ldb, d.K, d.M, d.N, i0, j0, 1.0, lds, t, wr, wc, lane, acc);
+  const double alpha = d.vscale ? d.alpha * sc->v : d.alpha;
+  const double vv = d.Y ? sc->v : 0.0;
+  // Epilogue through LDS, one half tile (64 rows) at a time: the two waves of that half store
+  // their accumulators (static indices: a rolled epilogue over the accumulators put them in
+  // scratch), then every thread finishes 16 rows x 2 adjacent columns -- whole-row (coalesced)
+  // accesses to C and the epilogue operands.
   double part = 0.0, part2 = 0.0;
+  constexpr int ES = TM;  // [64][128] doubles = 64 KB of the 68 KB staging array
+  for (int h = 0; h < 2; ++h) {
+    if (wr == h) {
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
+      for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
+        for (int y = 0; y < 4; ++y)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = i0 + 64 * wr + 16 * x + (lane >> 4) + 4 * r;
-        const int col = j0 + 64 * wc + 16 * y + (lane & 15);
-        if (row < d.M && col < d.N) {
+          for (int r = 0; r < 4; ++r)
+            lds[(16 * x + (lane >> 4) + 4 * r) * ES + 64 * wc + 16 * y + (lane & 15)] = acc[x][y][r];
+    }
+    __syncthreads();
+    const int col0 = j0 + 2 * (t & 63);
+    for (int i = 0; i < 16; ++i) {
+      const int lr = (t >> 6) + 4 * i, row = i0 + 64 * h + lr;
+      if (row >= d.M) break;  // (rows ascend with i)
+#pragma unroll
+      for (int e2 = 0; e2 < 2; ++e2) {
+        const int col = col0 + e2;
+        if (col < d.N) {
           const EpiIn e = epi_fetch(d, row, col);
-          const double c = epi_apply(d, alpha * acc[x][y][r], e, part, part2);
+          double c = alpha * lds[lr * ES + 2 * (t & 63) + e2];
+          if (d.Cp) c += d.Cp[(size_t)row * d.ldcp + col];
+          c = epi_apply(d, c, e, part, part2);
           d.C[(size_t)row * d.ldc + col] = c;
           epi_side(d, row, col, c, e, vv);
         }
       }
-    asm volatile("" ::: "memory");  // keep the epilogue's operand loads to one row block at a time
+    }
+    __syncthreads();
   }
   if (d.red) {
     double s = block_sum_256(part, sred);
@@ -661,37 +679,64 @@ __global__ __launch_bounds__(256) void gemm_huge_kernel(GemmBatch batch, const S
 }
 
 typedef void (*HugeFn)(GemmBatch, const StepScalars*, int);
-static HugeFn huge_fn(int sig) {
-  static const HugeFn tab[16] = {
-      gemm_huge_kernel<0, 0, 0, 0>, gemm_huge_kernel<0, 0, 0, 1>, gemm_huge_kernel<0, 0, 1, 0>,
-      gemm_huge_kernel<0, 0, 1, 1>, gemm_huge_kernel<0, 1, 0, 0>, gemm_huge_kernel<0, 1, 0, 1>,
-      gemm_huge_kernel<0, 1, 1, 0>, gemm_huge_kernel<0, 1, 1, 1>, gemm_huge_kernel<1, 0, 0, 0>,
-      gemm_huge_kernel<1, 0, 0, 1>, gemm_huge_kernel<1, 0, 1, 0>, gemm_huge_kernel<1, 0, 1, 1>,
-      gemm_huge_kernel<1, 1, 0, 0>, gemm_huge_kernel<1, 1, 0, 1>, gemm_huge_kernel<1, 1, 1, 0>,
-      gemm_huge_kernel<1, 1, 1, 1>};
-  return tab[sig & 15];
-}
-static int huge_sig(const GemmDesc& d) {
-  const int ta2 = d.K2 ? d.ta2 : 0, tb2 = d.K2 ? d.tb2 : 0;
-  return (d.ta ? 8 : 0) | (d.tb ? 4 : 0) | (ta2 ? 2 : 0) | (tb2 ? 1 : 0);
+static HugeFn huge_fn(int ta, int tb) {
+  static const HugeFn tab[4] = {gemm_huge_kernel<0, 0>, gemm_huge_kernel<0, 1>, gemm_huge_kernel<1, 0>,
+                                gemm_huge_kernel<1, 1>};
+  return tab[(ta ? 2 : 0) | (tb ? 1 : 0)];
 }
 
-// one launch per transpose signature present in the batch
+// one launch per transpose signature in each of two passes: pass 0 the first products of the
+// dual descriptors (plain stores: C = alpha op(A) op(B) [+ beta C0]), pass 1 every descriptor's
+// last product with its epilogue (a dual descriptor's second product reads pass 0's C as Cp).
 static hipError_t launch_huge(const GemmDesc* descs, int ndesc, const StepScalars* sc, hipStream_t s) {
-  bool done[GEMM_MAX_BATCH] = {};
+  GemmDesc pass[2][GEMM_MAX_BATCH];
+  int np[2] = {0, 0};
   for (int i = 0; i < ndesc; ++i) {
-    if (done[i]) continue;
-    const int sig = huge_sig(descs[i]);
-    GemmBatch b{};
-    int nb = 0, mt = 0;
-    for (int j = i; j < ndesc; ++j)
-      if (!done[j] && huge_sig(descs[j]) == sig) {
-        done[j] = true;
-        b.d[nb++] = descs[j];
-        mt = std::max(mt, gemm_tiles(descs[j], GEMM_HUGE));
-      }
-    const int per = (mt + 7) / 8;
-    hipLaunchKernelGGL(huge_fn(sig), dim3(8 * per, nb), dim3(256), 0, s, b, sc, per);
+    const GemmDesc& d = descs[i];
+    if (!d.K2) {
+      pass[1][np[1]++] = d;
+      continue;
+    }
+    // the second pass reads C while writing it (same element, same thread: read before write);
+    // C must not be an operand of the second product
+    if (d.C == d.A2 || d.C == d.B2 || d.C == d.F || d.C == d.U || d.C == d.Q1 || d.C == d.Q2 || d.C == d.Ys)
+      return hipErrorInvalidValue;
+    // nor may another descriptor of the batch read it (pass 0 writes it before pass 1 runs)
+    for (int j = 0; j < ndesc; ++j) {
+      const GemmDesc& o = descs[j];
+      if (j != i && (o.A == d.C || o.B == d.C || o.A2 == d.C || o.B2 == d.C || o.C0 == d.C || o.F == d.C ||
+                     o.U == d.C || o.Q1 == d.C || o.Q2 == d.C || o.Ys == d.C))
+        return hipErrorInvalidValue;
+    }
+    GemmDesc a{};  // alpha op(A) op(B) [+ beta C0] -> C
+    a.A = d.A; a.lda = d.lda; a.ta = d.ta; a.B = d.B; a.ldb = d.ldb; a.tb = d.tb;
+    a.alpha = d.alpha; a.vscale = d.vscale; a.C = d.C; a.ldc = d.ldc;
+    a.M = d.M; a.N = d.N; a.K = d.K; a.epi = EPI_STORE; a.gate = d.gate; a.ngate = d.ngate; a.tag = d.tag;
+    if (d.epi != EPI_RESID && d.beta != 0.0) { a.beta = d.beta; a.C0 = d.C0; a.ldc0 = d.ldc0; }
+    pass[0][np[0]++] = a;
+    GemmDesc b = d;  // alpha2 op(A2) op(B2) + C, then the descriptor's epilogue
+    b.A = d.A2; b.lda = d.lda2; b.ta = d.ta2; b.B = d.B2; b.ldb = d.ldb2; b.tb = d.tb2; b.K = d.K2;
+    b.alpha = d.alpha2; b.vscale = d.vscale2; b.K2 = 0; b.A2 = b.B2 = nullptr;
+    b.Cp = d.C; b.ldcp = d.ldc;
+    if (d.epi != EPI_RESID) b.beta = 0.0;
+    pass[1][np[1]++] = b;
+  }
+  for (int p = 0; p < 2; ++p) {
+    bool done[GEMM_MAX_BATCH] = {};
+    for (int i = 0; i < np[p]; ++i) {
+      if (done[i]) continue;
+      const int ta = pass[p][i].ta, tb = pass[p][i].tb;
+      GemmBatch b{};
+      int nb = 0, mt = 0;
+      for (int j = i; j < np[p]; ++j)
+        if (!done[j] && pass[p][j].ta == ta && pass[p][j].tb == tb) {
+          done[j] = true;
+          b.d[nb++] = pass[p][j];
+          mt = std::max(mt, gemm_tiles(pass[p][j], GEMM_HUGE));
+        }
+      const int per = (mt + 7) / 8;
+      hipLaunchKernelGGL(huge_fn(ta, tb), dim3(8 * per, nb), dim3(256), 0, s, b, sc, per);
+    }
   }
   return hipGetLastError();
 }
@@ -704,11 +749,7 @@ int gemm_tiles(const GemmDesc& d, int variant) {
 }
 
 int gemm_variant(const GemmDesc* descs, int ndesc, int force_big) {
-  if (force_big == 2) {
-    for (int i = 0; i < ndesc; ++i)
-      if (descs[i].K2 && descs[i].alpha == 0.0) return GEMM_BIG;
-    return GEMM_HUGE;
-  }
+  if (force_big == 2) return GEMM_HUGE;
   if (force_big) return GEMM_BIG;
   long tot16 = 0, tot128 = 0;
   for (int i = 0; i < ndesc; ++i) {
@@ -716,8 +757,6 @@ int gemm_variant(const GemmDesc* descs, int ndesc, int force_big) {
     tot128 += (long)((descs[i].M + 127) / 128) * ((descs[i].N + 127) / 128);
   }
   if (gemm_use_small(tot16)) return GEMM_SMALL;
-  for (int i = 0; i < ndesc; ++i)  // the 128x128 kernel folds a dual product by alpha2 / alpha
-    if (descs[i].K2 && descs[i].alpha == 0.0) return GEMM_BIG;
   return tot128 >= GEMM_HUGE_MIN_TILES ? GEMM_HUGE : GEMM_BIG;
 }
 

@@ -11,7 +11,6 @@
 // see "row-sharded multi-GPU step" below.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
-#include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <atomic>
@@ -128,8 +127,6 @@ struct gpk_handle {
   int ttg = 0, tngpa = 0;
   std::vector<GemmDesc> hdescs;  // per-stage GEMM descriptors (kernel arguments)
   Stage st[kGemmStages];
-  rocblas_handle rb = nullptr;   // the plain products of 128x128-tile stages (lib_plain)
-  bool gd_v = false;             // G_D stored without its v (a plain product), v in the contraction
   double *Kc[2] = {}, *pst[2] = {};  // kept K (refinement residuals), pivot stats (gate)
   unsigned int* aflag[2] = {};        // assembly -> pivot-0 hand-off counters (small path) /
                                       // update -> pivot hand-off counters (large path)
@@ -422,73 +419,9 @@ static void gemv_operand(const gpk_handle* h, GemvDesc& g) {
 
 static int enqueue_step_shard(gpk_handle* h, int apply);
 
-// A plain product -- one product C = alpha op(A) op(B) [+ beta C0], host-constant alpha and
-// beta, no refinement gate, epilogue, partial sums or side output -- of a stage that runs on
-// the 128x128-tile kernel is a plain library GEMM: rocBLAS (deterministic: atomics off by
-// default), which outruns gemm_huge_kernel on these shapes (tools/dgemm_library.py, 4096^3:
-// 67.8 / 74.1 / 73.3 TF/s NN / TN / NT against ~64).  The fused stages and the v-scaled products
-// (alpha * v, v on the device: rocBLAS's device pointer mode returned an internal error here)
-// stay on our kernels.
-static bool lib_plain(const GemmDesc& g) {
-  return g.epi == EPI_STORE && !g.gate && !g.Y && !g.red && !g.red2 && g.K2 == 0 && !g.vscale &&
-         !g.vscale2;
-}
-static int lib_gemm(gpk_handle* h, const GemmDesc& g) {
-  const rocblas_operation oa = g.ta ? rocblas_operation_transpose : rocblas_operation_none;
-  const rocblas_operation ob = g.tb ? rocblas_operation_transpose : rocblas_operation_none;
-  const double alpha = g.alpha, beta = g.C0 ? g.beta : 0.0;
-  const double* c = g.C0 ? g.C0 : g.C;
-  const int ldc = g.C0 ? g.ldc0 : g.ldc;
-  // row-major C = op(A) op(B) is column-major C^T = op(B)^T op(A)^T: B first, M and N swapped
-  const rocblas_status st = rocblas_gemm_ex(
-      h->rb, ob, oa, g.N, g.M, g.K, &alpha, g.B, rocblas_datatype_f64_r, g.ldb, g.A,
-      rocblas_datatype_f64_r, g.lda, &beta, c, rocblas_datatype_f64_r, ldc, g.C, rocblas_datatype_f64_r,
-      g.ldc, rocblas_datatype_f64_r, rocblas_gemm_algo_standard, 0, 0);
-  if (st != rocblas_status_success)
-    return fail(GPK_EHIP, std::string("rocblas_gemm_ex: ") + rocblas_status_to_string(st));
-  return GPK_OK;
-}
 static int launch_stage(gpk_handle* h, int k) {
-  const GemmDesc* ds = h->hdescs.data() + h->st[k].off;
-  const int n = h->st[k].n;
-  if (!h->rb || h->st[k].variant != GEMM_HUGE)
-    return check_launch(launch_gemm_auto(ds, n, h->sc, h->s, h->st[k].variant), "gemm");
-  GemmDesc rest[GEMM_MAX_BATCH];
-  int nr = 0;
-  for (int i = 0; i < n; ++i) {
-    if (lib_plain(ds[i])) {
-      TRY(lib_gemm(h, ds[i]));
-    } else {
-      rest[nr++] = ds[i];
-    }
-  }
-  if (nr) return check_launch(launch_gemm_auto(rest, nr, h->sc, h->s, GEMM_HUGE), "gemm");
-  return GPK_OK;
-}
-// rocBLAS for the plain products of 128x128-tile stages (unsharded 2D handles; GPK_NO_LIB_GEMM
-// set in the environment keeps every product on gemm_huge_kernel).  The workspace is preset and
-// every library product runs once here, outside any capture: no allocation or code-object load
-// inside a step graph's capture.  (The warm calls write only stage outputs every step rewrites.)
-static int setup_lib_gemm(gpk_handle* h) {
-  if (std::getenv("GPK_NO_LIB_GEMM")) return GPK_OK;
-  std::vector<int> plain;
-  for (int k = 0; k < kGemmStages; ++k)
-    if (h->st[k].variant == GEMM_HUGE)
-      for (int i = h->st[k].off; i < h->st[k].off + h->st[k].n; ++i)
-        if (lib_plain(h->hdescs[i])) plain.push_back(i);
-  if (plain.empty()) return GPK_OK;
-  if (rocblas_create_handle(&h->rb) != rocblas_status_success) return fail(GPK_EHIP, "rocblas_create_handle");
-  if (rocblas_set_stream(h->rb, h->s) != rocblas_status_success ||
-      rocblas_set_pointer_mode(h->rb, rocblas_pointer_mode_host) != rocblas_status_success)
-    return fail(GPK_EHIP, "rocblas handle setup");
-  constexpr size_t kWs = size_t(64) << 20;
-  void* ws = nullptr;
-  HIPCHK(hipMalloc(&ws, kWs));
-  h->allocs.push_back(ws);
-  if (rocblas_set_workspace(h->rb, ws, kWs) != rocblas_status_success) return fail(GPK_EHIP, "rocblas_set_workspace");
-  for (int i : plain) TRY(lib_gemm(h, h->hdescs[i]));
-  HIPCHK(hipStreamSynchronize(h->s));
-  return GPK_OK;
+  return check_launch(launch_gemm_auto(h->hdescs.data() + h->st[k].off, h->st[k].n, h->sc, h->s, h->st[k].variant),
+                      "gemm");
 }
 
 static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
@@ -522,7 +455,6 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
       pa[a].kc = h->kc + a;
       pa[a].GK = h->GK[a];
       pa[a].GD = h->GD[a];
-      pa[a].gd_v = h->gd_v ? 1 : 0;
       pa[a].deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
       pa[a].cls = h->cls[a];
@@ -738,14 +670,11 @@ static int build_descs(gpk_handle* h) {
     d.push_back(mk(h->R, P2, 0, h->D[1], P2, 0, h->T2, P2, P1, P2, P2));
   }
   {
-    // large unsharded factors: G_D / v, a plain product (lib_plain: rocBLAS with a host alpha);
-    // the contraction multiplies its G_D weights by v (PGradArgs::gd_v)
-    h->gd_v = h->bigspd && !h->shard && !std::getenv("GPK_NO_LIB_GEMM");
     GemmDesc g = mk(h->R, P2, 0, h->A, P2, 1, h->GD[0], P1, P1, P1, P2);
-    g.alpha = beta; g.vscale = h->gd_v ? 0 : 1;
+    g.alpha = beta; g.vscale = 1;
     d.push_back(g);
     GemmDesc g2 = mk(h->R, P2, 1, h->Bt, P2, 0, h->GD[1], P2, P2, P2, P1);
-    g2.vscale = h->gd_v ? 0 : 1;
+    g2.vscale = 1;
     d.push_back(g2);
   }
   end(6);
@@ -1686,7 +1615,6 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   }
   if (L.dim == 2 && (rc = build_descs(h)) != GPK_OK) return bail(rc);
   if (shard && (rc = build_shard(h)) != GPK_OK) return bail(rc);
-  if (L.dim == 2 && !shard && (rc = setup_lib_gemm(h)) != GPK_OK) return bail(rc);
   // (the 2D large-factor path has no refinement stages: its one graph is the fast one)
   h->fast_ok = !shard && !(h->bigspd && L.dim == 2) && !(p->flags & GPK_FLAG_NO_FAST_GRAPH);
   h->fast_mode = h->fast_ok && (p->flags & GPK_FLAG_FAST_FIRST);
@@ -1867,7 +1795,6 @@ int gpk_destroy(gpk_handle* h) {
   for (int k = 0; k <= kMaxStages; ++k)
     if (h->ev[k]) (void)hipEventDestroy(h->ev[k]);
   if (h->rep_host) (void)hipHostFree(h->rep_host);
-  if (h->rb) (void)rocblas_destroy_handle(h->rb);
   for (void* p : h->allocs) (void)hipFree(p);
   if (h->s) (void)hipStreamDestroy(h->s);
   delete h->comm;
@@ -2747,7 +2674,6 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
       pa[a] = PGradArgs{};
       pa[a].x = a == 0 ? h->x1 : h->x2; pa[a].n = a == 0 ? L.n1 : L.n2; pa[a].p = a == 0 ? L.p1 : L.p2;
       pa[a].kc = h->kc + a; pa[a].GK = h->GK[a]; pa[a].GD = h->GD[a]; pa[a].deriv = deriv;
-      pa[a].gd_v = h->gd_v ? 1 : 0;
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
       pa[a].cls = h->cls[a];
     }
@@ -2772,6 +2698,81 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
   *alg_flops = flops;
   *alg_bytes = bytes;
   return read_status(h);
+}
+
+int gpk_dgemm(int32_t variant, int32_t M, int32_t N, int32_t K, double alpha, const double* A,
+              int32_t lda, int32_t ta, const double* B, int32_t ldb, int32_t tb, int32_t K2,
+              double alpha2, const double* A2, int32_t lda2, int32_t ta2, const double* B2,
+              int32_t ldb2, int32_t tb2, double beta, const double* C0, double* C, int32_t ldc,
+              int32_t iters, double* avg_us) {
+  if (variant < 0 || variant > 3 || M <= 0 || N <= 0 || K <= 0 || K2 < 0 || (M | N | K | K2) & 31 ||
+      !A || !B || !C || (K2 && (!A2 || !B2)) || iters < 0 || (iters && !avg_us))
+    return fail(GPK_EINVAL, "gpk_dgemm: bad argument (M, N, K, K2 multiples of 32)");
+  // stored extents of op(A) = M x K etc.: rows x row length, each row length <= its ld
+  auto ext = [](int rows, int cols, int t, int ld, size_t* n) {
+    const int r = t ? cols : rows, c = t ? rows : cols;
+    *n = (size_t)(r - 1) * ld + c;
+    return ld >= c;
+  };
+  size_t na = 0, nb = 0, na2 = 0, nb2 = 0, nc = 0;
+  if (!ext(M, K, ta, lda, &na) || !ext(K, N, tb, ldb, &nb) || !ext(M, N, 0, ldc, &nc) ||
+      (K2 && (!ext(M, K2, ta2, lda2, &na2) || !ext(K2, N, tb2, ldb2, &nb2))))
+    return fail(GPK_EINVAL, "gpk_dgemm: leading dimension shorter than a row");
+  TRY(check_device(0));
+  DevSwitch dsw(0);
+  std::vector<void*> mem;
+  auto cleanup = [&]() { for (void* p : mem) (void)hipFree(p); };
+  auto up = [&](const double* src, size_t n, double** dst) -> hipError_t {
+    hipError_t e = hipMalloc(dst, n * 8);
+    if (e != hipSuccess) return e;
+    mem.push_back(*dst);
+    return src ? hipMemcpy(*dst, src, n * 8, hipMemcpyHostToDevice) : hipSuccess;
+  };
+  GemmDesc d{};
+  double *dA = nullptr, *dB = nullptr, *dA2 = nullptr, *dB2 = nullptr, *dC = nullptr, *dC0 = nullptr;
+  hipError_t e = up(A, na, &dA);
+  if (e == hipSuccess) e = up(B, nb, &dB);
+  if (e == hipSuccess && K2) e = up(A2, na2, &dA2);
+  if (e == hipSuccess && K2) e = up(B2, nb2, &dB2);
+  if (e == hipSuccess) e = up(C0 == C ? C : nullptr, nc, &dC);
+  if (e == hipSuccess && C0 && C0 != C) e = up(C0, nc, &dC0);
+  if (e != hipSuccess) {
+    cleanup();
+    return fail(e == hipErrorOutOfMemory ? GPK_ENOMEM : GPK_EHIP, std::string("gpk_dgemm: ") + hipGetErrorString(e));
+  }
+  d.A = dA; d.lda = lda; d.ta = ta ? 1 : 0; d.B = dB; d.ldb = ldb; d.tb = tb ? 1 : 0;
+  d.A2 = dA2; d.lda2 = lda2; d.ta2 = ta2 ? 1 : 0; d.B2 = dB2; d.ldb2 = ldb2; d.tb2 = tb2 ? 1 : 0;
+  d.alpha = alpha; d.alpha2 = alpha2; d.K2 = K2;
+  d.beta = C0 ? beta : 0.0; d.C0 = C0 ? (C0 == C ? dC : dC0) : nullptr; d.ldc0 = ldc;
+  d.C = dC; d.ldc = ldc; d.M = M; d.N = N; d.K = K; d.epi = EPI_STORE;
+  const int v = variant ? variant : gemm_variant(&d, 1, 0);
+  auto launch = [&]() { return launch_gemm_auto(&d, 1, nullptr, 0, v); };
+  // (an in-place C0 == C update is checked once; timed launches then repeat it on their own output)
+  e = launch();
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(C, dC, nc * 8, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && iters) {
+    hipEvent_t e0, e1;
+    e = hipEventCreate(&e0);
+    if (e == hipSuccess) {
+      e = hipEventCreate(&e1);
+      if (e == hipSuccess) {
+        (void)launch();  // warm
+        (void)hipEventRecord(e0, 0);
+        for (int it = 0; it < iters && e == hipSuccess; ++it) e = launch();
+        (void)hipEventRecord(e1, 0);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        float ms = 0.f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+        *avg_us = ms * 1000.0 / iters;
+        (void)hipEventDestroy(e1);
+      }
+      (void)hipEventDestroy(e0);
+    }
+  }
+  cleanup();
+  if (e != hipSuccess) return fail(GPK_EHIP, std::string("gpk_dgemm: ") + hipGetErrorString(e));
+  return GPK_OK;
 }
 
 }  // extern "C"

@@ -312,6 +312,9 @@ struct GemmDesc {
   // (S/2 + v X) formed where X is produced, so the G_K stage is a single product
   double* Y; const double* Ys; int ldy;
   int tag;                  // step stage (timeline probes only, gpk_trace.h)
+  // 128x128-tile kernel only: a partial product added to alpha op(A) op(B) before the epilogue
+  // (the first pass of a dual product, launch_gemm_auto's split)
+  const double* Cp; int ldcp;
 };
 constexpr int GEMM_MAX_BATCH = 4;
 struct GemmBatch {  // passed by value (kernarg): no dependent descriptor load before the operands
@@ -367,7 +370,6 @@ struct PGradArgs {
   const double* x; int n; int p;
   const AxisConst* kc;
   const double* GK; const double* GD;     // 2D mode: materialised [p*p]
-  int gd_v;                               // 1: GD holds G_D / v (library products), v applied here
   const double* Kinv;                     // 1D mode
   const double* alpha; const double* beta; const double* R;  // 1D mode vectors
   double halfc;                           // 1D mode: 0.5*logdet flag

@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
       const bool ok = u < C.ncls;
       sd[t] = ok ? C.dist[u] : 0.0;
       swk[t] = ok ? a : 0.0;
-      swd[t] = ok ? (A.gd_v ? d * sc->v : d) : 0.0;
+      swd[t] = ok ? d : 0.0;
     }
   } else if (t < PAIRS) {  // stage pair t
     int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
@@ -473,7 +473,6 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
         wk = gkij + gkji;
         wd = gdij + gdji;
       }
-      if (A.gd_v) wd *= sc->v;
     }
     sd[t] = d;
     swk[t] = wk;

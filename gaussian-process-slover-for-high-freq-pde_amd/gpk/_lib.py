@@ -127,6 +127,10 @@ EXPORTS = {
     "gpk_get_params3": ([ctypes.c_void_p, _dp, ctypes.c_int64], ctypes.c_int),
     "gpk_loss_grad3": ([ctypes.c_void_p, _dp, _dp], ctypes.c_int),
     "gpk_step3": ([ctypes.c_void_p, ctypes.c_int32, _dp], ctypes.c_int),
+    "gpk_dgemm": ([ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, _dp,
+                   ctypes.c_int32, ctypes.c_int32, _dp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                   ctypes.c_double, _dp, ctypes.c_int32, ctypes.c_int32, _dp, ctypes.c_int32, ctypes.c_int32,
+                   ctypes.c_double, _dp, _dp, ctypes.c_int32, ctypes.c_int32, _dp], ctypes.c_int),
     "gpk_trace_reset": ([], ctypes.c_int),
     "gpk_trace_read": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                         ctypes.c_int32], ctypes.c_int),
@@ -165,3 +169,28 @@ def dptr(a):
 
 def f64(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+GEMM_AUTO, GEMM_SMALL, GEMM_BIG, GEMM_TILE128 = 0, 1, 2, 3
+
+
+def dgemm(A, B, ta=False, tb=False, alpha=1.0, A2=None, B2=None, ta2=False, tb2=False, alpha2=1.0,
+          beta=0.0, C0=None, variant=GEMM_AUTO, iters=0):
+    """The step's fp64 MFMA GEMM kernels (gpk_dgemm) on host arrays: returns (C, avg_us) with
+    C = alpha op(A) op(B) [+ alpha2 op(A2) op(B2)] [+ beta C0]; avg_us is the average device time
+    of `iters` back-to-back launches (None when iters = 0).  Dimensions must be multiples of 32."""
+    A, B = f64(A), f64(B)
+    M, K = (A.shape[1], A.shape[0]) if ta else A.shape
+    N = B.shape[0] if tb else B.shape[1]
+    C = np.zeros((M, N)) if C0 is None else f64(C0).copy()
+    K2, pa2, pb2, lda2, ldb2 = 0, None, None, 1, 1
+    if A2 is not None:
+        A2, B2 = f64(A2), f64(B2)
+        K2 = A2.shape[0] if ta2 else A2.shape[1]
+        pa2, pb2, lda2, ldb2 = dptr(A2), dptr(B2), A2.shape[1], B2.shape[1]
+    us = ctypes.c_double(0.0)
+    check(load().gpk_dgemm(variant, M, N, K, alpha, dptr(A), A.shape[1], int(ta), dptr(B), B.shape[1],
+                           int(tb), K2, alpha2, pa2, lda2, int(ta2), pb2, ldb2, int(tb2), beta,
+                           dptr(C) if C0 is not None else None, dptr(C), N, iters,
+                           ctypes.byref(us) if iters else None))
+    return C, (us.value if iters else None)

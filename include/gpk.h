@@ -264,6 +264,20 @@ int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us);
 int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg_us,
                      double* alg_flops, double* alg_bytes);
 
+/* The step's fp64 MFMA GEMM kernels on host operands (row-major, device 0), for tests and
+ * rate measurements: C = alpha op(A) op(B) + alpha2 op(A2) op(B2) + beta C0, op = transpose
+ * when ta / tb / ta2 / tb2; K2 = 0 drops the second product; C0 may equal C (in-place
+ * update) or be NULL.  variant: 0 auto (the step's size rule), 1 16x16 latency tiles, 2 64x64
+ * tiles, 3 the 128x128 pipelined tile (model_GP_solver_2d.py:104-119's solves and products
+ * are these GEMMs here).  M, N, K, K2 multiples of 32 (the step's padding contract); lda etc.
+ * in elements.  iters > 0 times that many back-to-back launches with HIP events after the
+ * checked one and returns the average microseconds in *avg_us (may be NULL when iters = 0). */
+int gpk_dgemm(int32_t variant, int32_t M, int32_t N, int32_t K, double alpha, const double* A,
+              int32_t lda, int32_t ta, const double* B, int32_t ldb, int32_t tb, int32_t K2,
+              double alpha2, const double* A2, int32_t lda2, int32_t ta2, const double* B2,
+              int32_t ldb2, int32_t tb2, double beta, const double* C0, double* C, int32_t ldc,
+              int32_t iters, double* avg_us);
+
 /* ---- Row-sharded 2D step across GPUs (the reference has no multi-GPU path).
  * Every rank holds the problem, forms both Kronecker factors' K, D, K^{-1} itself, and computes
  * its block of rows of every product of the step (model_GP_solver_2d.py:87-183 /

@@ -96,10 +96,8 @@ int main(int argc, char** argv) {
       CHK(hipDeviceSynchronize());
       CHK(hipMemcpy(hr.data(), R, nn * 8, hipMemcpyDeviceToHost));
       struct V { const char* name; TileFn fn; } vs[] = {
-          {"tile prio1 sched", tile_fn<1, true>(ta, tb)},
-          {"tile prio0 sched", tile_fn<0, true>(ta, tb)},
-          {"tile prio1 nosch", tile_fn<1, false>(ta, tb)},
-          {"tile prio3 sched", tile_fn<3, true>(ta, tb)},
+          {"tile regs sched ", tile_fn<0, true>(ta, tb)},
+          {"tile regs nosch ", tile_fn<0, false>(ta, tb)},
       };
       for (const V& v : vs) {
         CHK(hipMemset(C, 0, nn * 8));
