@@ -171,21 +171,30 @@ def large_factors(steps=3):
                                      if stages.get("assemble") else None}}}
 
 
-def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
+def sharded_section(a, ctx, configs=("C4", "C5", "C5_split"), make_sharded=None, make_single=None):
     """ONE problem per config row-sharded over all ranks (gpk/shard.py: rows of every product
     per rank, RCCL all-gathers / all-reduces inside the step graph).  value = steps/s of the
     single problem (strong scaling).  C5_split: one Kronecker factor inverted per rank half,
-    broadcast over RCCL (GPK_FLAG_SPLIT_FACTORS) instead of both factors on every rank."""
-    from gpk import replicas, shard
-    from gpk._lib import GPK_FLAG_SPLIT_FACTORS
-    from gpk.problems import make_solver
+    broadcast over RCCL (GPK_FLAG_SPLIT_FACTORS) instead of both factors on every rank.
+    make_sharded(cid, flags) / make_single(cid): solver factories (the dry run passes stand-ins,
+    so the launcher tests run this very code on CPU)."""
+    from gpk import replicas
+    if make_sharded is None:
+        from gpk import shard
+        from gpk._lib import GPK_FLAG_SPLIT_FACTORS
+        from gpk.problems import make_solver
+        make_sharded = lambda cid, flags: shard.make_sharded_solver(cid, ctx, seed=0, flags=flags)  # noqa: E731
+        make_single = lambda cid: make_solver(cid, seed=0)  # noqa: E731
+        split_flag = GPK_FLAG_SPLIT_FACTORS
+    else:
+        split_flag = 1
     out, single = {}, {}
     for key in configs:
         cid = key.split("_")[0]
-        flags = GPK_FLAG_SPLIT_FACTORS if key.endswith("_split") else 0
+        flags = split_flag if key.endswith("_split") else 0
         steps = a.sharded_steps if cid == "C4" else max(2, a.sharded_steps // 10)
         STAGE["name"] = f"sharded {key}: create"
-        s = shard.make_sharded_solver(cid, ctx, seed=0, flags=flags)
+        s = make_sharded(cid, flags)
         try:
             STAGE["name"] = f"sharded {key}: prepare + warm-up"
             s.prepare(steps)
@@ -205,7 +214,7 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split")):
                     "steps": steps, "ranks": ctx.world}
         if cid not in single:
             STAGE["name"] = f"sharded {key}: single-GPU reference on rank 0"
-            single[cid] = single_gpu_reference(lambda: make_solver(cid, seed=0), steps, ctx)
+            single[cid] = single_gpu_reference(lambda: make_single(cid), steps, ctx)
         out[key].update(single[cid])
         out[key]["speedup_vs_1gpu"] = single[cid]["single_gpu_ms_per_step"] / out[key]["ms_per_step"]
     # C5 is reported both ways: both factors inverted on every rank, or one factor
@@ -235,27 +244,30 @@ def single_gpu_reference(make, steps, ctx):
             ms = (time.perf_counter() - t0) / steps * 1e3
         finally:
             s.close()
-    replicas.barrier(ctx)
+    # every rank gets rank 0's time (the others contribute 0 to the MAX): each rank computes the
+    # same speedup and leaves the section together
+    ms = replicas.max_over_ranks(ms if ms is not None else 0.0, ctx)
     return {"single_gpu_ms_per_step": ms, "single_gpu_steps": steps}
 
 
 def dry_run_sharded_section(a, ctx):
-    """--dry-run --dry-run-sharded ok|hang|raise: a stand-in for sharded_section with the same
-    barrier / max-over-ranks plumbing; 'hang' blocks rank 1 (a stuck collective), 'raise' fails
-    rank 1.  Tests check that bench.py then exits non-zero."""
-    from gpk import replicas
-    STAGE["name"] = "dry-run sharded: timed steps"
-    if ctx.rank == 1 and a.dry_run_sharded == "hang":
-        time.sleep(3600)
-    if ctx.rank == 1 and a.dry_run_sharded == "raise":
-        raise RuntimeError("stand-in collective failed")
-    replicas.barrier(ctx)
-    dt = replicas.max_over_ranks(1e-3, ctx)
-    out = {"value": 1.0 / dt, "unit": "iters/s", "ms_per_step": dt * 1e3, "ranks": ctx.world}
-    out.update(single_gpu_reference(lambda: _DryRunSolver(0), 3, ctx))
-    out["speedup_vs_1gpu"] = (out["single_gpu_ms_per_step"] / out["ms_per_step"]
-                              if out["single_gpu_ms_per_step"] is not None else None)
-    return {"dry-run": out}
+    """--dry-run --dry-run-sharded ok|hang|raise: sharded_section itself on stand-in solvers
+    (same barriers, max-over-ranks, single-GPU reference and speedup on every rank); 'hang'
+    blocks rank 1's timed steps (a stuck collective), 'raise' fails them.  Tests check that
+    bench.py exits 0 on every rank for 'ok' and non-zero otherwise."""
+    mode = a.dry_run_sharded
+
+    class Sharded(_DryRunSolver):
+        def step(self, n):
+            if ctx.rank == 1 and mode == "hang" and n > 2:
+                time.sleep(3600)
+            if ctx.rank == 1 and mode == "raise" and n > 2:
+                raise RuntimeError("stand-in collective failed")
+            return super().step(n)
+
+    return sharded_section(a, ctx, configs=("C4", "C5_split"),
+                           make_sharded=lambda cid, flags: Sharded(ctx.rank),
+                           make_single=lambda cid: _DryRunSolver(0))
 
 
 def kernel_roofline(s, cfg, iters):
@@ -360,6 +372,8 @@ def main():
     ap.add_argument("--no-large", action="store_true", help="skip the C5-size MFMA section")
     ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the row-sharded section")
     ap.add_argument("--sharded-steps", type=int, default=50)
+    ap.add_argument("--train-warmup", type=int, default=200,
+                    help="Adam steps before the train_regime timing (after the timed batch)")
     ap.add_argument("--sharded-timeout", type=float, default=240.0)
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/rank plumbing only: gloo, stand-in solver, no GPU (tests)")
@@ -401,6 +415,21 @@ def main():
 
     extra = {}
     if not a.dry_run:
+        # the training regime (model_GP_solver_2d.py:285-332 runs nepoch steps): the same
+        # step(K) call after >= 200 more Adam steps, with the graph it ran on (the refinement gate
+        # follows the params, so the first 25 steps alone do not show a long run's rate)
+        s.step(a.train_warmup)
+        s.sync()
+        tr_fast, tr_rb0 = s.graph_mode()
+        t = time.perf_counter()
+        s.step(a.steps)
+        s.sync()
+        dtr = time.perf_counter() - t
+        tr_fast_end, tr_rb1 = s.graph_mode()
+        extra["train_regime"] = {"value": a.steps / dtr, "unit": "iters/s", "ms_per_step": dtr / a.steps * 1e3,
+                                 "steps": a.steps, "after_steps": a.warmup + a.steps + a.train_warmup,
+                                 "step_graph": {"fast": bool(tr_fast), "fast_at_end": bool(tr_fast_end),
+                                                "rollbacks": int(tr_rb1 - tr_rb0)}}
         # the reference's loop shape: one step() call per iteration (model_GP_solver_2d.py:285-300)
         s.step(5)
         s.sync()
@@ -504,6 +533,7 @@ def emit(a, value, dt, world, fast_graph, fast_end, rollbacks, final_loss, path,
         "roofline": extra.get("roofline"),
         "kernels_us": extra.get("kernels_us"),
         "assembly": extra.get("assembly"),
+        "train_regime": extra.get("train_regime"),
         "step1_per_call": extra.get("step1_per_call"),
         "cpu_baseline": extra.get("cpu_baseline"),
         "cpu_baseline_1core": extra.get("cpu_baseline_1core"),

@@ -305,6 +305,7 @@ static hipError_t launch_inverse(gpk_handle* h, SpdArgs* sa, double** fin, bool 
 }
 
 static int split_broadcast(gpk_handle* h);  // (after ShardComm)
+static int status_allreduce(gpk_handle* h);
 
 // assemble K, D (+ step constants, + pivot block 0) and invert K: the first part of a step
 static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
@@ -586,8 +587,8 @@ static int build_descs(gpk_handle* h) {
   // Accuracy of each choice against the long-double yardstick: tests/test_gpu_accuracy.py,
   // profiles/r3_parity.json, DESIGN.md §5.
   const int rfl = h->prob.flags;
-  const bool ref_fwd = !h->bigspd || !(rfl & GPK_FLAG_NO_REFINE);
-  const bool ref_rev = !h->bigspd || ((rfl & GPK_FLAG_REFINE_ALL) && !(rfl & GPK_FLAG_NO_REFINE));
+  const bool ref_fwd = !(rfl & GPK_FLAG_NO_REFINE);
+  const bool ref_rev = (!h->bigspd || (rfl & GPK_FLAG_REFINE_ALL)) && !(rfl & GPK_FLAG_NO_REFINE);
   bool ref_now = ref_fwd;
   auto pushg = [&](const GemmDesc& g) {
     if (ref_now) d.push_back(g);
@@ -605,6 +606,10 @@ static int build_descs(gpk_handle* h) {
     d.push_back(mk(h->Up, P2, 0, h->Kinv[1], P2, 0, h->Bt, P2, P1, P2, P2));
   }
   end(0);
+  // (Measured in C4's training regime, tools/train_regime_parity.py, profiles/r5_train_regime_
+  // parity.json: with the gate closed -- cond(K) <= 1.4e3, bound < 21 -- the unrefined step is
+  // within 0.45 of the parity bar on its own K and D after 200-2000 Adam steps; refining the
+  // forward solves every step took that to 0.05-0.25 for ~12 us per step, so the gate stays.)
   begin(1);  // residuals W1 = U - K1 A, W2 = U - Bt K2
   {
     GemmDesc g = mk(h->Kc[0], P1, 0, h->A, P2, 0, h->W1, P2, P1, P2, P1);
@@ -922,13 +927,18 @@ static int split_broadcast(gpk_handle* h) {
     TRY(h->comm->broadcast(h, h->ldet[b], (size_t)P / 32, root));
     TRY(h->comm->broadcast(h, h->pst[b], 2, root));
   }
-  // a non-PD factor (or a hand-off timeout) is seen on device by the ranks that inverted it
-  // only: sum the status bits over the group so that every rank returns GPK_ENOTPD -- a rank
-  // that carried on would enter the next step's collectives alone and hang
+  return GPK_OK;
+}
+
+// Every sharded step, after the inverse: the device status bits summed over the group.  A
+// non-PD factor under the split is seen only by the ranks that inverted it, and a hand-off
+// timeout (bit 2) is rank-local by nature (one rank's wait gave up); with the bits group-wide
+// every rank fails the batch and undoes it (its snapshot) together -- a rank that carried on
+// would enter the next step's collectives alone and hang, or keep params its peers dropped.
+static int status_allreduce(gpk_handle* h) {
   TRY(check_launch(launch_status_f64(h->status, h->stat_x, 0, h->s), "status_pack"));
   TRY(h->comm->allreduce(h, h->stat_x, 2));
-  TRY(check_launch(launch_status_f64(h->status, h->stat_x, 1, h->s), "status_unpack"));
-  return GPK_OK;
+  return check_launch(launch_status_f64(h->status, h->stat_x, 1, h->s), "status_unpack");
 }
 
 // Row slices of the step's GEMM stages for this rank, the variant per stage (its tile rows must
@@ -994,6 +1004,7 @@ static int build_shard(gpk_handle* h) {
 static int enqueue_step_shard(gpk_handle* h, int apply) {
   const Layout& L = h->L;
   TRY(enqueue_assemble_inverse(h, apply));  // replicated: K, D, K^{-1}, log det, step constants
+  TRY(status_allreduce(h));                  // a failed inverse fails every rank's batch
   for (int k = 0; k < kGemmStages; ++k) {
     if (h->sst[k].n)  // (empty: a refinement stage of a path without refinement)
       TRY(check_launch(launch_gemm_auto(h->sdescs.data() + h->sst[k].off, h->sst[k].n, h->sc, h->s,
@@ -1194,12 +1205,13 @@ static int read_status(gpk_handle* h) {
 
 // End of a batch (one synchronisation): non-positive-definite status, the fast graph's gate
 // violation flag, and the refinement gate of the last step, which picks the next batch's graph:
-// the fast one once max_a K00 * max diag K_a^{-1} is 8x below REFINE_COND_LB, and it stays
+// the fast one once max_a K00 * max diag K_a^{-1} is 2x below REFINE_COND_LB, and it stays
 // the fast one while that bound stays below REFINE_COND_LB itself (hysteresis: a fast batch
 // that crosses the gate is caught by the check in the fast graph's tail (viol) and rerun, which
-// costs one FAST_CHUNK; leaving the fast graph at the 8x margin cost ~15% on every later step
-// of C4's training, whose bound drifts into that band and stays there).
-constexpr double FAST_GRAPH_MARGIN = 8.0;
+// costs one FAST_CHUNK; leaving the fast graph at the margin cost ~15% on every later step of
+// C4's training, whose bound drifts to ~21 (tools/train_regime_parity.py): round 4's 8x entry
+// margin (12.5) kept a handle that had left the fast graph off it for ~2000 steps).
+constexpr double FAST_GRAPH_MARGIN = 2.0;
 static int read_report(gpk_handle* h, bool fast, bool* violated);
 
 // params, Adam state and step count back to the snapshot the current batch's begin took (every
@@ -1691,7 +1703,11 @@ static int group_run(gpk_handle** hs, int nranks, int apply, int n_steps) {
     th.emplace_back([&, r]() {
       gpk_handle* h = hs[r];
       DevSwitch ds(h->dev);
-      int rc = hipMemsetAsync(h->loss_slot, 0, sizeof(int), h->s) == hipSuccess ? GPK_OK : GPK_EHIP;
+      // the batch begin: loss slot reset and the snapshot a failed batch is undone to
+      StepBegin b{};
+      b.snap = h->snap; b.params = h->params; b.m = h->m; b.v = h->v; b.np = (size_t)h->L.nparams;
+      b.snap_count = h->snap_count; b.count = h->count; b.loss_slot = h->loss_slot;
+      int rc = check_launch(launch_step_begin(b, h->s), "step_begin");
       for (int i = 0; i < n_steps && rc == GPK_OK; ++i) rc = enqueue_step_shard(h, apply);
       if (rc == GPK_OK && hipStreamSynchronize(h->s) != hipSuccess) rc = fail(GPK_EHIP, "group step sync");
       if (rc != GPK_OK) {
@@ -1703,11 +1719,10 @@ static int group_run(gpk_handle** hs, int nranks, int apply, int n_steps) {
   for (auto& t : th) t.join();
   for (int r = 0; r < nranks; ++r)
     if (rcs[r] != GPK_OK) return fail(rcs[r], "rank " + std::to_string(r) + ": " + errs[r]);
-  // every rank's status: a group whose ranks disagree about a non-PD factor would, under RCCL,
-  // leave the reporting ranks out of the next step's collectives -- the step makes that status
-  // group-wide (split_broadcast), so such a disagreement is an internal error.  A hand-off
-  // timeout (bit 2) is rank-local by nature (a wait of one rank's launch gave up): it fails the
-  // whole group with GPK_ENOTPD, and every rank's hand-off slots are reset.
+  // every rank's status: the step makes it group-wide (status_allreduce), so ranks that disagree
+  // are an internal error.  A failed batch (non-PD factor, or a hand-off timeout: bit 2, raised by
+  // one rank's wait and summed over the group) fails the whole group with GPK_ENOTPD; every rank
+  // resets its hand-off slots and restores the batch's snapshot.
   std::vector<int> st(nranks, 0);
   int any = 0, bad = 0;
   for (int r = 0; r < nranks; ++r) {
@@ -1717,10 +1732,11 @@ static int group_run(gpk_handle** hs, int nranks, int apply, int n_steps) {
     bad += st[r] != 0;
   }
   if (!any) return GPK_OK;
-  for (int r = 0; r < nranks; ++r) {
+  for (int r = 0; r < nranks; ++r) {  // every rank undoes the batch (gpk.h: failed batches are undone)
     DevSwitch ds(hs[r]->dev);
     HIPCHK(hipMemsetAsync(hs[r]->status, 0, sizeof(int), hs[r]->s));
     if (any & 2) TRY(reset_handoffs(hs[r]));
+    TRY(restore_snapshot(hs[r]));
     HIPCHK(hipStreamSynchronize(hs[r]->s));
   }
   if (any & 2) {
@@ -1989,8 +2005,12 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
     return read_report(h, false, &viol);
   }
   while (done < n_steps) {
+    // (both graphs run in FAST_CHUNK chunks while the fast graph is available, so the mode is
+    // re-decided every 64 steps: a long first call on the full graph used to keep its whole
+    // length there, and the training that followed, until the gate bound fell below the entry
+    // margin -- round 4's W = 200 line at 8100 it/s)
     const bool fast = h->fast_ok && h->fast_mode;
-    const int n = fast ? std::min(FAST_CHUNK, n_steps - done) : n_steps - done;
+    const int n = h->fast_ok ? std::min(FAST_CHUNK, n_steps - done) : n_steps - done;
     double* lo = losses ? losses + done : nullptr;
     bool viol = false;
     auto cg = fast && !h->shard ? h->g_calln.find(n) : h->g_calln.end();
@@ -2363,12 +2383,20 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
   const int64_t n1 = L.n1, n2 = L.n2;
   int64_t want;
   if (L.dim == 2) {
-    const int64_t sizes[6] = {n1 * n1, n2 * n2, n1 * n2, n2 * n1, n1 * n2, n1 * n2};
-    if (what < 0 || what > 5) return fail(GPK_EINVAL, "what must be 0..5 (2D)");
+    const int64_t sizes[22] = {n1 * n1, n2 * n2, n1 * n2, n2 * n1, n1 * n2, n1 * n2,
+                               n1 * n1, n1 * n1, n2 * n2, n2 * n2, n1 * n1, n2 * n2,
+                               n1 * n1, n2 * n2, n1 * n2, n1 * n2, n1 * n2, n1 * n2,
+                               n1 * n1, n2 * n2, n1 * n1, n2 * n2};
+    if (what < 0 || what > 21) return fail(GPK_EINVAL, "what must be 0..21 (2D)");
+    if ((what == 18 || what == 19) && !h->Kc[what - 18])
+      return fail(GPK_EINVAL, "this handle keeps no copy of K");
+    if ((what == 12 || what == 13) && !h->PD[what - 12])
+      return fail(GPK_EINVAL, "K^{-1} D^T is formed on the augmented chain path only");
     want = sizes[what];
   } else {
-    if (what != 0 && what != 2 && what != 4) return fail(GPK_EINVAL, "what must be 0, 2 or 4 (1D)");
-    want = what == 0 ? n1 * n1 : n1;
+    if (what != 0 && what != 2 && what != 4 && what != 6 && what != 7)
+      return fail(GPK_EINVAL, "what must be 0, 2, 4, 6 or 7 (1D)");
+    want = (what == 0 || what >= 6) ? n1 * n1 : n1;
   }
   if (n != want) return fail(GPK_EINVAL, "output size mismatch");
   DevSwitch ds(h->dev);
@@ -2393,6 +2421,30 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
   }
   double loss = 0.0;
   TRY(gpk_loss_grad(h, &loss, nullptr));  // device buffers now hold the forward quantities
+  if (L.dim == 1 && what >= 6) {  // the step's K (6) and D (7), as its last step assembled them
+    const int P = L.p1, na = L.n1;
+    const ClassArgs& C = h->cls[0];
+    if (C.ncls > 0) {  // class ids + class values (K and D are never materialised on this path)
+      std::vector<int> cid((size_t)P * P);
+      std::vector<double> cv(C.ncls);
+      HIPCHK(hipMemcpy(cid.data(), C.cid, cid.size() * sizeof(int), hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpy(cv.data(), what == 6 ? C.kval : C.dval, cv.size() * sizeof(double), hipMemcpyDeviceToHost));
+      for (int i = 0; i < na; ++i)
+        for (int j = 0; j < na; ++j) {
+          double v = cv[cid[(size_t)i * P + j]];
+          if (what == 6 && i == j) v += h->prob.jitter;  // (the gather adds it per element)
+          out[(size_t)i * na + j] = v;
+        }
+      return GPK_OK;
+    }
+    const double* m = what == 6 ? h->Kc[0] : h->D[0];
+    if (!m) return fail(GPK_EINVAL, "this handle keeps no copy of K / D");
+    host.resize((size_t)P * P);
+    HIPCHK(hipMemcpy(host.data(), m, host.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int i = 0; i < na; ++i)
+      for (int j = 0; j < na; ++j) out[(size_t)i * na + j] = host[(size_t)i * P + j];
+    return GPK_OK;
+  }
   if (L.dim == 1) {
     const int P = L.p1;
     const double* src = h->alpha;
@@ -2413,6 +2465,29 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
     return GPK_OK;
   }
   const int P1 = L.p1, P2 = L.p2;
+  if ((what >= 6 && what <= 13) || what >= 18) {  // work matrices, K^{-1}, K^{-1} D^T, Kc, D (P x P)
+    const int a = (what == 6 || what == 7 || what == 10 || what == 12 || what == 18 || what == 20) ? 0 : 1;
+    const int P = a == 0 ? P1 : P2, na = a == 0 ? L.n1 : L.n2;
+    const double* m = what >= 20 ? h->D[a] : what >= 18 ? h->Kc[a] : what >= 12 ? h->PD[a]
+                    : what >= 10 ? h->Kinv[a] : (what == 6 || what == 8) ? h->GK[a] : h->GD[a];
+    host.resize((size_t)P * P);
+    hipError_t e = hipMemcpyAsync(host.data(), m, host.size() * sizeof(double), hipMemcpyDeviceToHost, h->s);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->s);
+    if (e != hipSuccess) return fail(GPK_EHIP, hipGetErrorString(e));
+    for (int i = 0; i < na; ++i)
+      for (int j = 0; j < na; ++j) out[(size_t)i * na + j] = host[(size_t)i * P + j];
+    return GPK_OK;
+  }
+  if (what >= 14) {  // grid work matrices R, X1, X2, S (P1 x P2)
+    const double* m = what == 14 ? h->R : what == 15 ? h->X1 : what == 16 ? h->X2 : h->S;
+    host.resize((size_t)P1 * P2);
+    hipError_t e = hipMemcpyAsync(host.data(), m, host.size() * sizeof(double), hipMemcpyDeviceToHost, h->s);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->s);
+    if (e != hipSuccess) return fail(GPK_EHIP, hipGetErrorString(e));
+    for (int64_t i = 0; i < n1; ++i)
+      for (int64_t j = 0; j < n2; ++j) out[i * n2 + j] = host[(size_t)i * P2 + j];
+    return GPK_OK;
+  }
   const double* src = (what == 3) ? h->Bt : h->A;
   if (what >= 4) {  // U_xx = D1 A  /  U_yy = Bt D2^T
     HIPCHK(hipMalloc(&tmp, (size_t)P1 * P2 * sizeof(double)));

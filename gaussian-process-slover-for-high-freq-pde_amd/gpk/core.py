@@ -223,18 +223,25 @@ class DeviceSolver:
         check(_lib.load().gpk_criterion(self._h, ctypes.byref(c)))
         return c.value
 
-    FIELDS_2D = {"K1": 0, "K2": 1, "K1inv_U": 2, "K2inv_Ut": 3, "U_xx": 4, "U_yy": 5}
-    FIELDS_1D = {"K": 0, "Kinv_u": 2, "u_xx": 4}
+    FIELDS_2D = {"K1": 0, "K2": 1, "K1inv_U": 2, "K2inv_Ut": 3, "U_xx": 4, "U_yy": 5,
+                 "G_K1": 6, "G_D1": 7, "G_K2": 8, "G_D2": 9, "K1inv": 10, "K2inv": 11,
+                 "K1inv_D1t": 12, "K2inv_D2t": 13, "R": 14, "X1": 15, "X2": 16, "S": 17,
+                 "Kc1": 18, "Kc2": 19, "D1": 20, "D2": 21}
+    FIELDS_1D = {"K": 0, "Kinv_u": 2, "u_xx": 4, "Kc": 6, "D": 7}
 
     def forward_field(self, name):
         """value_and_grad_kernel quantities at the current params, computed on the device."""
         if self.dim == 2:
             what = self.FIELDS_2D[name]
             shape = [(self.n1, self.n1), (self.n2, self.n2), (self.n1, self.n2),
-                     (self.n2, self.n1), (self.n1, self.n2), (self.n1, self.n2)][what]
+                     (self.n2, self.n1), (self.n1, self.n2), (self.n1, self.n2),
+                     (self.n1, self.n1), (self.n1, self.n1), (self.n2, self.n2), (self.n2, self.n2),
+                     (self.n1, self.n1), (self.n2, self.n2), (self.n1, self.n1), (self.n2, self.n2),
+                     (self.n1, self.n2), (self.n1, self.n2), (self.n1, self.n2), (self.n1, self.n2),
+                     (self.n1, self.n1), (self.n2, self.n2), (self.n1, self.n1), (self.n2, self.n2)][what]
         else:
             what = self.FIELDS_1D[name]
-            shape = (self.n1, self.n1) if what == 0 else (self.n1, 1)
+            shape = (self.n1, self.n1) if what in (0, 6, 7) else (self.n1, 1)
         out = np.empty(shape)
         check(_lib.load().gpk_forward_field(self._h, what, dptr(out), out.size))
         return out
@@ -353,6 +360,15 @@ class DeviceGroup(DeviceSolver):
         mu, nu = f64(mu).reshape(-1), f64(nu).reshape(-1)
         for k in range(self.nranks):
             check(_lib.load().gpk_set_opt_state(self._hs[k], int(count), dptr(mu), dptr(nu), self.nparams))
+
+    def rank_state(self, k):
+        """(flat params, Adam count, mu, nu) held by rank k's handle."""
+        lib = _lib.load()
+        flat, mu, nu = np.empty(self.nparams), np.empty(self.nparams), np.empty(self.nparams)
+        cnt = ctypes.c_int64()
+        check(lib.gpk_get_params(self._hs[k], dptr(flat), self.nparams))
+        check(lib.gpk_get_opt_state(self._hs[k], ctypes.byref(cnt), dptr(mu), dptr(nu), self.nparams))
+        return flat, cnt.value, mu, nu
 
     def loss_grad(self):
         loss = ctypes.c_double()

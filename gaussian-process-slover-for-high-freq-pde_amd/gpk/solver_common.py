@@ -162,11 +162,24 @@ class SolverBase(object):
         count, mu, nu = self.dev.get_opt_state()
         arrs = {"params": self.dev.get_flat(), "count": np.int64(count), "mu": mu, "nu": nu}
         if loop is not None:
-            done, min_err, inc, log = loop
-            arrs.update(done=np.int64(done), min_err=np.float64(min_err), inc=np.int64(inc))
+            done, min_err, inc, log = loop[:4]
+            stopped = loop[4] if len(loop) > 4 else -1
+            arrs.update(done=np.int64(done), min_err=np.float64(min_err), inc=np.int64(inc),
+                        early_stop_epoch=np.int64(stopped))
             for k, v in log.items():
                 arrs["log_" + k] = np.asarray(v)
-        np.savez(path, **arrs)
+        # written to a temporary file in the same directory and renamed onto `path` (exactly that
+        # name: a file object keeps np.savez from appending ".npz"): a job killed mid-write leaves
+        # the previous checkpoint intact
+        import os
+        tmp = "%s.tmp.%d" % (path, os.getpid())
+        try:
+            with open(tmp, "wb") as f:
+                np.savez(f, **arrs)
+            os.replace(tmp, path)
+        finally:
+            if os.path.exists(tmp):
+                os.remove(tmp)
 
     def load_checkpoint(self, path):
         """Restore a save_checkpoint() file onto the device; returns the train-loop state or None."""
@@ -178,7 +191,8 @@ class SolverBase(object):
                 return None
             # (per-record arrays stay arrays, scalars Python numbers: as train() appends them)
             log = {k[4:]: [x.copy() if x.ndim else x.item() for x in z[k]] for k in z.files if k.startswith("log_")}
-            return int(z["done"]), float(z["min_err"]), int(z["inc"]), log
+            stopped = int(z["early_stop_epoch"]) if "early_stop_epoch" in z else -1
+            return int(z["done"]), float(z["min_err"]), int(z["inc"]), log, stopped
 
     def train(self, nepoch, seed=0, verbose=True, checkpoint=None, resume=None, stop_at=None, perf_log=None):
         """train() (model_GP_solver_2d.py:235-352): same records, same early-stopping rule.
@@ -202,7 +216,11 @@ class SolverBase(object):
             st = self.load_checkpoint(resume)
             if st is None:
                 raise ValueError("resume: %s holds no train-loop state" % resume)
-            done, min_err, error_increase_count, log = st
+            done, min_err, error_increase_count, log, stopped = st
+            if stopped >= 0:  # the checkpointed run had stopped early: nothing left to train
+                early_stopping = {"flag": True, "epoch": stopped}
+                self.params = self.current().to_dict()
+                return self._finish_log(log), early_stopping, min_err
         rec = record_epochs(nepoch)
         bar = _tqdm.tqdm(total=nepoch, initial=done, disable=not verbose) if _tqdm is not None else None
         for i in rec + [nepoch]:
@@ -239,15 +257,19 @@ class SolverBase(object):
                 with open(perf_log, "a") as f:
                     f.write(json.dumps({"epoch": i, "loss": loss, "err": float(err), "criterion": float(criterion),
                                         "steps": int(n), "seconds": dt, "steps_per_s": n / dt if dt > 0 else None}) + "\n")
+            # the early-stop rule first (the uninterrupted run's order), and its outcome goes into
+            # the checkpoint: a run resumed from this record stops exactly where it did
+            stop = (self.early_stop_enabled and self.trick_paras.get("tol", -1) > 0
+                    and criterion < self.trick_paras["tol"])
             if checkpoint is not None:
-                self.save_checkpoint(checkpoint, (done, min_err, error_increase_count, log))
-            if stop_at is not None and done >= stop_at:
-                break
-            if self.early_stop_enabled and self.trick_paras.get("tol", -1) > 0 and criterion < self.trick_paras["tol"]:
+                self.save_checkpoint(checkpoint, (done, min_err, error_increase_count, log, i if stop else -1))
+            if stop:
                 if verbose:
                     print("early stop at epoch %d" % i)
                 early_stopping["flag"] = True
                 early_stopping["epoch"] = i
+                break
+            if stop_at is not None and done >= stop_at:
                 break
         if bar is not None:
             bar.close()

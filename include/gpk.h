@@ -84,7 +84,7 @@ typedef struct gpk_problem {
 #define GPK_FLAG_FORCE_HUGE_GEMM 8 /* use the 128x128 throughput GEMM at every size (tests/tuning) */
 /* gpk_step / gpk_loss_grad run one of two captured step graphs: the full one, whose iterative-
  * refinement GEMM stages check a device-side cond(K) gate and skip themselves when it is closed,
- * or a fast one without those stages, chosen while the last observed gate value is 8x below its
+ * or a fast one without those stages, chosen while the last observed gate value is 2x below its
  * threshold.  The fast graph checks the gate every step; a step that needed refinement makes the
  * call roll its batch back (params, Adam state) and rerun it with the full graph, so results are
  * bitwise those of the full graph. */
@@ -117,7 +117,8 @@ typedef struct gpk_problem {
 #define GPK_FLAG_FORCE_CHAIN_MULTI 4096 /* the macro-tile chain at every 1D size (tests) */
 /* Large 2D factors (P >= 1600): which solves get one (cond-gated) refinement step.  Default: the
  * forward solves A = K1^{-1} U, Bt = U K2^{-1}; REFINE_ALL: also S and X1 / X2 (every solve, as
- * the small-factor path); NO_REFINE: none (explicit-inverse products only). */
+ * the small-factor path, whose forward solves are refined on every step, ungated); NO_REFINE:
+ * none at any size (explicit-inverse products only; accuracy studies). */
 #define GPK_FLAG_REFINE_ALL 8192
 #define GPK_FLAG_NO_REFINE 16384
 /* Large 1D factors on the macro-tile chain: the inverse launch writes Kc and D as matrices and the
@@ -242,8 +243,14 @@ int gpk_criterion(gpk_handle* h, double* out);
 /* value_and_grad_kernel (model_GP_solver_2d.py:87-121 / model_GP_solver_1d.py:80-99) at the
  * current params, computed on the device; `what` selects one field, out gets it unpadded:
  *   2D: 0 K1 [n1*n1], 1 K2 [n2*n2], 2 K1inv_U [n1*n2], 3 K2inv_Ut [n2*n1], 4 U_xx [n1*n2],
- *       5 U_yy [n1*n2]   (advection: U_x, U_y)
- *   1D: 0 K [n*n], 2 Kinv_u [n], 4 u_xx [n]                                                */
+ *       5 U_yy [n1*n2]   (advection: U_x, U_y); the reverse pass's kernel-parameter operands
+ *       (diagnostics): 6 G_K1, 7 G_D1 [n1*n1], 8 G_K2, 9 G_D2 [n2*n2] (the weights of
+ *       sum_ij G_K dK/dtheta + G_D dD/dtheta), 10 K1^{-1} [n1*n1], 11 K2^{-1} [n2*n2],
+ *       12 K1^{-1} D1^T [n1*n1], 13 K2^{-1} D2^T [n2*n2] (augmented chain path only), 14 R,
+ *       15 X1, 16 X2, 17 S [n1*n2] (model_GP_solver_2d.py:133 residual),
+ *       18 Kc1, 19 Kc2 (the step's kept copy of K, refinement residuals), 20 D1, 21 D2 (the
+ *       step's derivative blocks) -- the matrices as the last step assembled them
+ *   1D: 0 K [n*n], 2 Kinv_u [n], 4 u_xx [n]; 6 K, 7 D [n*n] as the last step assembled them                                                */
 int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n);
 
 /* Per-stage device timings (HIP events on the handle's stream) of one step, averaged over

@@ -105,3 +105,47 @@ def test_preds_full_size_vs_oracle(cid):
     record_parity("test_preds_full_size_vs_oracle", cid, {"preds_rel_l2": e}, 1e-6,
                   {"m_test": 300, "max_abs_rel": rel(pd, po)})
     assert e < 1e-6, (cid, e)
+
+
+def test_training_regime_c4_on_step_fields():
+    """C4 after 1000 Adam steps (the regime a train() of nepoch steps spends its time in,
+    code/model_GP_solver_2d.py:285-332): cond(K) ~ 1e3 and the kernel-parameter gradient is
+    ill-conditioned in K and D.  Against the long-double yardstick on the step's OWN K and D
+    (gpk_forward_field Kc / D: the class-evaluated fields), loss and every gradient key stay
+    within max(1e-10, 4 x the fp64 LU oracle's distance on the same K and D).  (On the oracle's
+    K and D the device is ~2e-9 off in the kernel parameters -- and so is the LU oracle fed the
+    step's K and D: the ~1-ulp differences of two fp64 evaluations of the fields, amplified by
+    that conditioning; tools/train_regime_parity.py, profiles/r5_train_regime_parity.json.)
+    Also: the step ran on the fast graph (gate closed, no rollback)."""
+    from gpk.problems import make_solver
+    import tools.solve_accuracy as SA
+    O.set_backend(True)
+    prob, params0, _, _ = config_problem("C4")
+    s = make_solver("C4", seed=0)
+    try:
+        s.step(1000)
+        s.sync()
+        fast, _ = s.graph_mode()
+        flat = s.get_flat()
+        loss, g = s.loss_grad()
+        fields = {n: s.forward_field(n) for n in ("Kc1", "D1", "Kc2", "D2")}
+    finally:
+        s.close()
+    assert fast
+    params = O.unflatten_params(params0, flat)
+    kd = {id(params["kernel_paras_1"]): (fields["Kc1"], fields["D1"]),
+          id(params["kernel_paras_2"]): (fields["Kc2"], fields["D2"])}
+    saved = O.kernel_kd
+    O.kernel_kd = lambda kind, x, kp, jitter, dv: kd[id(kp)]
+    try:
+        ext = SA.run_mode(prob, params, "ext")
+        lu = SA.run_mode(prob, params, "lu")
+    finally:
+        O.kernel_kd = saved
+    gd = O.unflatten_params(params, g)
+    dev = SA.distances((loss, {k: O.flatten_params(gd[k]) for k in gd}), ext)
+    ref = SA.distances(lu, ext)
+    tol = {k: max(1e-10, 4 * v) for k, v in ref.items()}
+    record_parity("test_training_regime_c4_on_step_fields", "C4@1000", dev, tol, {"lu_oracle_err": ref})
+    for k, e in dev.items():
+        assert e < tol[k], (k, e, tol[k])

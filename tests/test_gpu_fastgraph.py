@@ -201,3 +201,23 @@ def test_many_single_step_calls_bitwise_one_long_call():
     finally:
         a.close()
         b.close()
+
+
+def test_long_first_call_then_fast_graph_c4():
+    """A handle's first call of 200 steps (round 4's bench with --warmup 200) starts on the full
+    graph, but both graphs now run in 64-step chunks while the fast one is available, so the mode
+    is re-decided every chunk: the next call runs on the fast graph.  Bitwise the same trajectory
+    as 200 steps in 5-step calls (the fast graph is bitwise the full one)."""
+    from gpk.problems import make_solver
+    a = make_solver("C4", seed=0)
+    b = make_solver("C4", seed=0)
+    try:
+        la = a.step(200)
+        fast_a, _ = a.graph_mode()
+        lb = np.concatenate([b.step(5) for _ in range(40)])
+        assert fast_a, "still on the full graph after a 200-step first call"
+        assert np.array_equal(la, lb)
+        assert np.array_equal(a.get_flat(), b.get_flat())
+    finally:
+        a.close()
+        b.close()

@@ -116,3 +116,37 @@ def test_group_timeout_is_enotpd(wait_limit):
         assert abs(lg - lo) / abs(lo) < 1e-9
     finally:
         g.close()
+
+
+def test_group_step_timeout_undone_on_every_rank(wait_limit):
+    """A hand-off timeout inside a group's step batch: the status bits are summed over the group
+    every sharded step (gpk_api.cpp status_allreduce), so every rank fails the batch and restores
+    its snapshot -- params and Adam state equal the pre-call state on every rank, the ranks agree,
+    and the next batch equals a group that never timed out."""
+    from gpk._lib import GPKError, GPK_ENOTPD
+    from tests.test_shard import _group
+    prob, params, _, fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=72, n2=64, Q=4, seed=8)
+    g = _group(prob, 4, fs, 2)
+    f = _group(prob, 4, fs, 2)
+    try:
+        g.set_params(params)
+        f.set_params(params)
+        g.step(2)
+        f.step(2)
+        before = [g.rank_state(k) for k in range(2)]
+        wait_limit(1)
+        with pytest.raises(GPKError) as ei:
+            g.step(3)
+        wait_limit(0)
+        assert ei.value.code == GPK_ENOTPD and "timed out" in str(ei.value), str(ei.value)
+        after = [g.rank_state(k) for k in range(2)]
+        for k in range(2):
+            assert _same_state(after[k], before[k]), f"rank {k}: the failed batch was not undone"
+        # (Adam moments of U are kept per rank for its own rows only; params and count are shared)
+        assert np.array_equal(after[0][0], after[1][0]) and after[0][1] == after[1][1], \
+            "the ranks disagree after the failed batch"
+        assert np.array_equal(g.step(3), f.step(3))
+        assert _same_state(g.rank_state(1), f.rank_state(1))
+    finally:
+        g.close()
+        f.close()
