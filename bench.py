@@ -43,22 +43,33 @@ KERNEL_LAUNCHES = {"spd_chain": 1, "sweep": None, "gemm_B": 3, "pgrad": 1, "asse
 
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench (tools/gpu_round.sh), summarised by
 # tools/pmc_summary.py: HBM-side bytes per launch (2*FETCH + WRITE, MI355X_MICROARCH.md §HBM)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r4_pmc_c4.json")
-if not os.path.exists(PMC_SUMMARY):
-    PMC_SUMMARY = os.path.join(ROOT, "profiles", "r2_pmc_c4.json")
+# (the newest round's summary; the line names it and the source tree it was measured on, so a
+# traffic figure older than the kernel it prices is visible as such)
+def _newest_pmc():
+    import glob
+    import re
+    files = glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_c4.json"))
+    files.sort(key=lambda f: int(re.match(r"r(\d+)_", os.path.basename(f)).group(1)))
+    return files[-1] if files else None
+
+
+PMC_SUMMARY = _newest_pmc()
 PMC_KERNEL = {"spd_chain": "gpk::chain_kernel<2, true>", "sweep": "gpk::sweep_kernel",
               "gemm_B": "gpk::gemm_small_kernel<true>", "pgrad": "gpk::pgrad_kernel<true, true, 2, false, true>",
               "assemble": "gpk::class_eval_kernel<true, true, 2>"}
 
 
 def pmc_traffic(kernel):
-    """Bytes per launch of `kernel` from the committed PMC summary (None if absent)."""
+    """(bytes per launch of `kernel` from the committed PMC summary or None, the summary's
+    provenance: file, the source tree it was measured on, how)."""
     try:
         with open(PMC_SUMMARY) as f:
-            k = json.load(f)["kernels"].get(kernel)
-        return None if k is None else k["traffic_bytes"]
-    except (OSError, ValueError, KeyError):
-        return None
+            d = json.load(f)
+        k = d["kernels"].get(kernel)
+        src = {"file": os.path.relpath(PMC_SUMMARY, ROOT), "tree": d.get("tree"), "how": d.get("source")}
+        return (None if k is None else k["traffic_bytes"]), src
+    except (OSError, ValueError, KeyError, TypeError):
+        return None, None
 
 
 # ------------------------------------------------------------------------------------------
@@ -292,7 +303,7 @@ def kernel_roofline(s, cfg, iters):
         roof = {"kernel": dom, "bound": "mfma", "achieved": d["flops"] / (d["us"] * 1e-6) / 1e12,
                 "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s"}
     roof["frac"] = roof["achieved"] / roof["peak"]
-    roof["traffic"] = pmc_traffic(PMC_KERNEL[dom])
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(PMC_KERNEL[dom])
     roof["avg_launch_us"] = d["us"]
     roof["alg_flops_per_launch"] = d["flops"]
     roof["alg_bytes_per_launch"] = d["bytes"]

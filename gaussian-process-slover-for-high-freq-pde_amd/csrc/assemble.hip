@@ -29,8 +29,8 @@ GPK_TRACE_TU(assemble)
 // Partial sums over components c = c0, c0 + cs, ... (cs = stride) of K and D at one pair.
 template <bool MATERN, bool COS, int DERIV>
 __device__ __forceinline__ void eval_kd_part(double diff, const double* w, const double* a,
-                                             const double* om, int c0, int cs, int q, double& K,
-                                             double& D) {
+                                             const double* om, const double* oml, int c0, int cs,
+                                             int q, double& K, double& D) {
   double d = fabs(diff);
   double k = 0.0, dv = 0.0;
   for (int c = c0; c < q; c += cs) {
@@ -38,7 +38,7 @@ __device__ __forceinline__ void eval_kd_part(double diff, const double* w, const
     radial<MATERN>(d, a[c], m0, m1, m2);
     if (COS) {
       double S, C;
-      sincos(om[c] * d, &S, &C);
+      phase_sincos(om[c], oml[c], d, S, C);
       double o = om[c];
       k += w[c] * (m0 * C);
       if (DERIV == 2) dv += w[c] * (m2 * C - 2.0 * m1 * (o * S) - m0 * (o * o * C));
@@ -55,8 +55,9 @@ __device__ __forceinline__ void eval_kd_part(double diff, const double* w, const
 
 template <bool MATERN, bool COS, int DERIV>
 __device__ __forceinline__ void eval_kd(double diff, const double* w, const double* a,
-                                        const double* om, int q, double& K, double& D) {
-  eval_kd_part<MATERN, COS, DERIV>(diff, w, a, om, 0, 1, q, K, D);
+                                        const double* om, const double* oml, int q, double& K,
+                                        double& D) {
+  eval_kd_part<MATERN, COS, DERIV>(diff, w, a, om, oml, 0, 1, q, K, D);
   // JAX abs JVP: select(x >= 0, g, -g) -> sign(0) = +1
   if (DERIV == 1 && !(diff >= 0.0)) D = -D;
 }
@@ -113,9 +114,9 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
   // issue priority over the other ~4 waves sharing each SIMD
   if (b.pivot_x >= 0 && (tile == 0 || pivot_wg)) __builtin_amdgcn_s_setprio(3);
 
-  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX], sol[QMAX];
   __shared__ double pk[4][64], pd[4][64];
-  if (t < q) axis_component(b.prep, axis, q, t, sw[t], sa[t], so[t]);
+  if (t < q) axis_component(b.prep, axis, q, t, sw[t], sa[t], so[t], sol[t]);
   if (blockIdx.x == 0 && axis == 0) publish_prep(b.prep, q);
   __syncthreads();
   if (pivot_wg) {
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(AssembleBatch b, int q) {
   double diff = 0.0, kv = 0.0, dv = 0.0;
   if (real) {
     diff = A.x[i] - A.x[j];
-    eval_kd_part<MATERN, COS, DERIV>(diff, sw, sa, so, g, 4, q, kv, dv);
+    eval_kd_part<MATERN, COS, DERIV>(diff, sw, sa, so, sol, g, 4, q, kv, dv);
   }
   pk[g][e] = kv;
   pd[g][e] = dv;
@@ -179,15 +180,15 @@ __global__ __launch_bounds__(256) void class_eval_kernel(AssembleBatch b, int q)
   const int axis = blockIdx.y;
   const ClassArgs& C = b.ax[axis].cls;
   const int t = threadIdx.x;
-  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
-  if (t < q) axis_component(b.prep, axis, q, t, sw[t], sa[t], so[t]);
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX], sol[QMAX];
+  if (t < q) axis_component(b.prep, axis, q, t, sw[t], sa[t], so[t], sol[t]);
   if (blockIdx.x == 0 && axis == 0) publish_prep(b.prep, q);
   __syncthreads();
   if (TR_FIRST) TR_LO(SLOT_CLASS_EVAL);
   if (TR_LAST) TR_LO(SLOT_CEVAL_START);
   const int c = t & 31, u = blockIdx.x * 8 + (t >> 5);
   double kv = 0.0, dv = 0.0;
-  if (u < C.ncls) eval_kd_part<MATERN, COS, DERIV>(C.dist[u], sw, sa, so, c, 32, q, kv, dv);
+  if (u < C.ncls) eval_kd_part<MATERN, COS, DERIV>(C.dist[u], sw, sa, so, sol, c, 32, q, kv, dv);
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) {
     kv += __shfl_xor(kv, o, 64);
@@ -270,6 +271,10 @@ __global__ __launch_bounds__(256) void gather_kernel(AssembleBatch b) {
 // rate (a pure write stream of the same bytes does not slow down: profiles/r4_gather_context.txt)
 constexpr int GW_H = 4, GW_ROWS = 4 * GW_H, GW_COLS = 512;
 constexpr int GW_WIDE_MIN_TILES = 1024;  // 32x32 tiles: P >= 1024
+struct GwIds {  // one block's class ids of a lane: variant bytes (2 columns) + their cbase entries
+  unsigned short v[GW_H][4];
+  int2 cb[GW_H][4];
+};
 // Persistent: GW_WGS workgroups walk the blocks (axis, row block, column block) with a stride of
 // the grid, and each issues the NEXT block's class ids before it gathers and stores the current
 // one, so the store stream does not stall on the id loads' HBM latency.
@@ -286,19 +291,25 @@ __global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b, int n
     const int p = axis ? b.ax[1].p : b.ax[0].p;
     return r0 < p && c0 < p;
   };
-  auto load_ids = [&](int2 (&id)[GW_H][4], int axis, int r0, int c0) {
-    const int* cid = axis ? b.ax[1].cls.cid : b.ax[0].cls.cid;
-    const int p = axis ? b.ax[1].p : b.ax[0].p;
+  // A pair's class is cbase[|i - j|] + its variant byte: the 2 bytes of a lane's column pair and
+  // the two cbase entries (n + 1 ints, cache-resident) are loaded together, the class values
+  // after them -- the id stream from HBM is 2 bytes per pair instead of round 4's 4-byte class
+  // ids (C5: 33 MB per gather instead of 134 MB)
+  auto load_ids = [&](GwIds& id, int axis, int r0, int c0) {
+    const ClassArgs& C = axis ? b.ax[1].cls : b.ax[0].cls;
+    const int p = axis ? b.ax[1].p : b.ax[0].p, n = axis ? b.ax[1].n : b.ax[0].n;
 #pragma unroll
     for (int h = 0; h < GW_H; ++h)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int col = c0 + 128 * q + 2 * lane;
-        id[h][q] = (col < p) ? *reinterpret_cast<const int2*>(cid + (size_t)(r0 + w + 4 * h) * p + col)
-                             : make_int2(-1, -1);
+        const int col = c0 + 128 * q + 2 * lane, i = r0 + w + 4 * h;
+        const bool in = col < p;
+        id.v[h][q] = in ? *reinterpret_cast<const unsigned short*>(C.vidx + (size_t)i * p + col) : 0xffff;
+        const int k0 = min(abs(i - col), n - 1), k1 = min(abs(i - col - 1), n - 1);
+        id.cb[h][q] = make_int2(C.cbase[k0], C.cbase[k1]);
       }
   };
-  auto process = [&](const int2 (&id)[GW_H][4], int axis, int r0, int c0) {
+  auto process = [&](const GwIds& ids, int axis, int r0, int c0) {
     const AssembleArgs& A = axis ? b.ax[1] : b.ax[0];
     const double* kval = A.cls.kval;
     const double* dval = A.cls.dval;
@@ -326,7 +337,8 @@ __global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b, int n
         double kv[2], dv[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-          const int u = e == 0 ? id[h][q].x : id[h][q].y, j = col[q] + e;
+          const int vb = (ids.v[h][q] >> (8 * e)) & 0xff;
+          const int u = vb == 0xff ? -1 : (e == 0 ? ids.cb[h][q].x : ids.cb[h][q].y) + vb, j = col[q] + e;
           if (u >= 0) {
             kv[e] = kval[u];
             if (i == j) kv[e] += A.jitter;
@@ -353,7 +365,7 @@ __global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b, int n
         if (DERIV) __builtin_nontemporal_store(d2, reinterpret_cast<d2v*>(A.D + o));
       }
   };
-  int2 ida[GW_H][4], idb[GW_H][4];
+  GwIds ida, idb;
   int blk = blockIdx.x, ax, r0, c0;
   while (blk < nblk && !where(blk, ax, r0, c0)) blk += gridDim.x;
   if (blk >= nblk) return;
@@ -375,6 +387,8 @@ __global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b, int n
 }
 
 static void launch_gather_wide(const AssembleBatch& b, int naxes, int deriv, hipStream_t s) {
+  for (int k = 0; k < naxes; ++k)
+    if (!b.ax[k].cls.vidx) return;  // (the handle builds them for p >= 1024; the launch fails below)
   int pmax = 0;
   for (int k = 0; k < naxes; ++k) pmax = std::max(pmax, b.ax[k].p);
   const int nbx = (pmax + GW_COLS - 1) / GW_COLS, nby = (pmax + GW_ROWS - 1) / GW_ROWS, nblk = nbx * nby * naxes;
@@ -431,19 +445,20 @@ __global__ __launch_bounds__(256) void cross_kernel(const double* __restrict__ x
                                                     const double* __restrict__ xc, int nc, int ld,
                                                     const AxisConst* kc, int q, double jitter,
                                                     double* K, double* D) {
-  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX], sol[QMAX];
   const int t = threadIdx.x;
   if (t < q) {
     sw[t] = kc->w[t];
     sa[t] = kc->a[t];
     so[t] = kc->om[t];
+    sol[t] = kc->oml[t];
   }
   __syncthreads();
   const int j = blockIdx.x * 64 + (t & 63);
   const int i = blockIdx.y * 4 + (t >> 6);
   if (i >= nr || j >= nc) return;
   double kv, dv;
-  eval_kd<MATERN, COS, DERIV>(xr[i] - xc[j], sw, sa, so, q, kv, dv);
+  eval_kd<MATERN, COS, DERIV>(xr[i] - xc[j], sw, sa, so, sol, q, kv, dv);
   if (i == j) kv += jitter;
   K[(size_t)i * ld + j] = kv;
   if (DERIV) D[(size_t)i * ld + j] = dv;
@@ -454,18 +469,19 @@ template <bool MATERN, bool COS, int DERIV>
 __global__ __launch_bounds__(256) void pairs_kernel(const double* __restrict__ x1,
                                                     const double* __restrict__ x2, long n,
                                                     const AxisConst* kc, int q, double* out) {
-  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX], sol[QMAX];
   const int t = threadIdx.x;
   if (t < q) {
     sw[t] = kc->w[t];
     sa[t] = kc->a[t];
     so[t] = kc->om[t];
+    sol[t] = kc->oml[t];
   }
   __syncthreads();
   const long e = (long)blockIdx.x * 256 + t;
   if (e >= n) return;
   double kv, dv;
-  eval_kd<MATERN, COS, DERIV>(x1[e] - x2[e], sw, sa, so, q, kv, dv);
+  eval_kd<MATERN, COS, DERIV>(x1[e] - x2[e], sw, sa, so, sol, q, kv, dv);
   out[e] = DERIV ? dv : kv;
 }
 

@@ -1298,6 +1298,7 @@ static void host_axis_const(const double* logw, const double* logls, const doubl
     kc->w[c] = std::exp(logw[c]);
     kc->a[c] = std::exp(logls[c]);
     kc->om[c] = TWO_PI * freq[c];
+    kc->oml[c] = om_low(freq[c], kc->om[c]);
   }
 }
 
@@ -1577,6 +1578,21 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
         return bail(fail(GPK_EHIP, "upload distance classes"));
       c.ncls = U; c.vmax = vmax[a]; c.dist = dist; c.cid = cid; c.cbase = cb;
       c.kval = kval; c.dval = dval; c.nchunk = nchunk; c.rb = rb; c.part = part;
+      if (P >= 1024) {  // the large-factor gather's variant bytes (ClassArgs::vidx)
+        std::vector<unsigned char> vb((size_t)P * P, 0xff);
+        for (int i = 0; i < n; ++i)
+          for (int j = 0; j < n; ++j) {
+            const int u = ccid[a][(size_t)i * P + j];
+            if (u >= 0) vb[(size_t)i * P + j] = (unsigned char)(u - cbase[a][std::abs(i - j)]);
+          }
+        unsigned char* dv = nullptr;
+        if (hipMalloc(&dv, vb.size()) != hipSuccess) return bail(fail(GPK_ENOMEM, "hipMalloc (class variants)"));
+        h->allocs.push_back(dv);
+        if (hipMemcpyAsync(dv, vb.data(), vb.size(), hipMemcpyHostToDevice, h->s) != hipSuccess ||
+            hipStreamSynchronize(h->s) != hipSuccess)
+          return bail(fail(GPK_EHIP, "upload class variants"));
+        c.vidx = dv;
+      }
     }
     h->bpa = std::max(pgrad_class_blocks(h->cls[0].ncls), L.dim == 2 ? pgrad_class_blocks(h->cls[1].ncls) : 0);
     h->cls_gemv = h->chain_multi && L.dim == 1 && !(p->flags & GPK_FLAG_MATRIX_GEMV);
@@ -2383,11 +2399,12 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
   const int64_t n1 = L.n1, n2 = L.n2;
   int64_t want;
   if (L.dim == 2) {
-    const int64_t sizes[22] = {n1 * n1, n2 * n2, n1 * n2, n2 * n1, n1 * n2, n1 * n2,
+    const int64_t sizes[26] = {n1 * n1, n2 * n2, n1 * n2, n2 * n1, n1 * n2, n1 * n2,
                                n1 * n1, n1 * n1, n2 * n2, n2 * n2, n1 * n1, n2 * n2,
                                n1 * n1, n2 * n2, n1 * n2, n1 * n2, n1 * n2, n1 * n2,
-                               n1 * n1, n2 * n2, n1 * n1, n2 * n2};
-    if (what < 0 || what > 21) return fail(GPK_EINVAL, "what must be 0..21 (2D)");
+                               n1 * n1, n2 * n2, n1 * n1, n2 * n2, n1 * n1, n2 * n2, n1 * n1, n2 * n2};
+    if (what < 0 || what > 25) return fail(GPK_EINVAL, "what must be 0..25 (2D)");
+    if (what >= 22 && h->cls[0].ncls <= 0) return fail(GPK_EINVAL, "this handle does not use distance classes");
     if ((what == 18 || what == 19) && !h->Kc[what - 18])
       return fail(GPK_EINVAL, "this handle keeps no copy of K");
     if ((what == 12 || what == 13) && !h->PD[what - 12])
@@ -2465,6 +2482,25 @@ int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n) {
     return GPK_OK;
   }
   const int P1 = L.p1, P2 = L.p2;
+  if (what >= 22) {  // K (22, 23) / D (24, 25) expanded on the host from the class table (cid + values)
+    const int a = (what == 22 || what == 24) ? 0 : 1;
+    const ClassArgs& C = h->cls[a];
+    const int P = a == 0 ? P1 : P2, na = a == 0 ? L.n1 : L.n2;
+    std::vector<int> cid((size_t)P * P);
+    std::vector<double> cv(C.ncls), x(na);
+    HIPCHK(hipMemcpy(cid.data(), C.cid, cid.size() * sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cv.data(), what <= 23 ? C.kval : C.dval, cv.size() * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(x.data(), a == 0 ? h->x1 : h->x2, na * sizeof(double), hipMemcpyDeviceToHost));
+    const bool sgn = what >= 24 && h->prob.eq == GPK_ADVECTION;  // D_x1: s_ij (JAX abs'(0) = +1)
+    for (int i = 0; i < na; ++i)
+      for (int j = 0; j < na; ++j) {
+        double v = cv[cid[(size_t)i * P + j]];
+        if (what <= 23 && i == j) v += h->prob.jitter;
+        if (sgn && !(x[i] - x[j] >= 0.0)) v = -v;
+        out[(size_t)i * na + j] = v;
+      }
+    return GPK_OK;
+  }
   if ((what >= 6 && what <= 13) || what >= 18) {  // work matrices, K^{-1}, K^{-1} D^T, Kc, D (P x P)
     const int a = (what == 6 || what == 7 || what == 10 || what == 12 || what == 18 || what == 20) ? 0 : 1;
     const int P = a == 0 ? P1 : P2, na = a == 0 ? L.n1 : L.n2;

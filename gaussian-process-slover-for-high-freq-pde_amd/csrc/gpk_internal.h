@@ -24,8 +24,45 @@ inline int pad_up(int n) { return (n + PADM - 1) / PADM * PADM; }
 struct AxisConst {
   double w[QMAX];    // e^{log-w}
   double a[QMAX];    // e^{log-ls}   (an inverse lengthscale, kernel_matrix.py:147)
-  double om[QMAX];   // 2*pi*freq
+  double om[QMAX];   // 2*pi*freq, rounded
+  double oml[QMAX];  // its rounding error: om + oml = 2*pi*freq exactly (om_low)
 };
+
+// The kernel fields with the phase and radial arguments as double-doubles.  fp64 rounds the
+// phase 2*pi*f*d (~250 rad at C5) and the radial argument sqrt5*a*d / a*d^2 by ~|arg| * eps, and
+// cos / sin / exp inherit that as an absolute error: hundreds of ulp in K, D and the derivative
+// fields, which the kernel-parameter contraction cancels into ~1e-8 relative at C5
+// (tools/c5_kp_split.py).  Carrying the argument's low part and correcting to first order
+// (cos(h + l) = cos h - l sin h, e^{-(h + l)} = e^{-h} (1 - l); l^2 ~ 1e-28) leaves the
+// sincos / exp rounding only: the fields to a few ulp of exact, for two FMAs per argument.
+__host__ __device__ inline double om_low(double freq, double om) { return fma(TWO_PI, freq, -om); }
+
+__device__ __forceinline__ void phase_sincos(double om, double oml, double d, double& S, double& C) {
+  const double h = om * d;
+  const double l = fma(om, d, -h) + oml * d;
+  double s, c;
+  sincos(h, &s, &c);
+  S = fma(l, c, s);
+  C = fma(-l, s, c);
+}
+
+// e^{-arg} of the radial factor and the argument's high part: Matern52 arg = sqrt5 a d,
+// SE arg = a d^2, both as double-doubles
+template <bool MATERN>
+__device__ __forceinline__ double radial_exp(double d, double a, double& r) {
+  double l;
+  if (MATERN) {
+    const double p = SQRT5 * a;
+    r = p * d;
+    l = fma(p, d, -r) + fma(SQRT5, a, -p) * d;
+  } else {
+    const double d2 = d * d;
+    r = a * d2;
+    l = fma(a, d2, -r) + a * fma(d, d, -d2);
+  }
+  const double E = exp(-r);
+  return fma(-l, E, E);
+}
 
 // Step scalars (device), written by the prep kernel.
 struct StepScalars {
@@ -36,13 +73,14 @@ struct StepScalars {
 // radial factor m(d) and derivatives; Matern52 (kernel_matrix.py:147-151) or SE (:125)
 template <bool MATERN>
 __device__ __forceinline__ void radial(double d, double a, double& m0, double& m1, double& m2) {
+  double r;
+  const double E = radial_exp<MATERN>(d, a, r);
   if (MATERN) {
-    double r = SQRT5 * a * d, E = exp(-r);
     m0 = (1.0 + r + r * r * (1.0 / 3.0)) * E;
     m1 = -(SQRT5 / 3.0) * a * r * (1.0 + r) * E;
     m2 = (5.0 / 3.0) * a * a * (r * r - r - 1.0) * E;
   } else {
-    double d2 = d * d, g = exp(-a * d2);
+    const double d2 = d * d, g = E;
     m0 = g;
     m1 = -2.0 * a * d * g;
     m2 = (4.0 * a * a * d2 - 2.0 * a) * g;
@@ -53,8 +91,9 @@ __device__ __forceinline__ void radial(double d, double a, double& m0, double& m
 template <bool MATERN>
 __device__ __forceinline__ void radial_l(double d, double a, double& m0, double& m1, double& m2,
                                          double& m0l, double& m1l, double& m2l) {
+  double r;
+  const double E = radial_exp<MATERN>(d, a, r);
   if (MATERN) {
-    double r = SQRT5 * a * d, E = exp(-r);
     double ka = (SQRT5 / 3.0) * a, k2 = (5.0 / 3.0) * a * a;
     double r2 = r * r;
     m0 = (1.0 + r + r2 * (1.0 / 3.0)) * E;
@@ -64,7 +103,7 @@ __device__ __forceinline__ void radial_l(double d, double a, double& m0, double&
     m1l = -ka * r * (2.0 + 2.0 * r - r2) * E;
     m2l = k2 * (-r2 * r + 5.0 * r2 - 2.0 * r - 2.0) * E;
   } else {
-    double d2 = d * d, g = exp(-a * d2);
+    const double d2 = d * d, g = E;
     m0 = g;
     m1 = -2.0 * a * d * g;
     m2 = (4.0 * a * a * d2 - 2.0 * a) * g;
@@ -123,6 +162,9 @@ struct ClassArgs {
   const double* dist;    // [ncls] d of each class
   const int* cid;        // [p*p] class of pair (i, j); -1 on pads
   const int* cbase;      // [n+1] first class of diagonal k
+  // [p*p] bytes: the variant of pair (i, j) on its diagonal, cid - cbase[|i - j|] (< CLS_VMAX),
+  // 255 on pads; built for the large-factor gather (p >= 1024), whose id stream it shrinks 4x
+  const unsigned char* vidx;
   double* kval;          // [ncls] kappa(d)      (+ jitter is added per element)
   double* dval;          // [ncls] d2k or |dk| (the D_x1 sign s_ij is applied per element)
   // hyper-parameter contraction: row chunk c of the class-sum launch writes its partial sums

@@ -57,6 +57,7 @@ __global__ __launch_bounds__(256) void k3_prep_kernel(K3Prep P) {
     for (int c = t; c < P.q; c += 256) {
       const int off = P.off_kp[ax];
       P.kc[ax].om[c] = TWO_PI * P.params[off + c];
+      P.kc[ax].oml[c] = om_low(P.params[off + c], P.kc[ax].om[c]);
       P.kc[ax].a[c] = exp(P.params[off + P.q + c]);
       P.kc[ax].w[c] = exp(P.params[off + 2 * P.q + c]);
     }

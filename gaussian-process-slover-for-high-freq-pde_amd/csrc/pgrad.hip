@@ -402,13 +402,14 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
   if (b.shard_n > 1 && tile % b.shard_n != b.shard_rank) return;
 
   __shared__ double sd[PAIRS], swk[PAIRS], swd[PAIRS];
-  __shared__ double sw[QMAX], sa[QMAX], so[QMAX];
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX], sol[QMAX];
   __shared__ double sacc[8][3][32];
   const int t = threadIdx.x;
   if (t < q) {
     sw[t] = A.kc->w[t];
     sa[t] = A.kc->a[t];
     so[t] = A.kc->om[t];
+    sol[t] = A.kc->oml[t];
   }
   constexpr int NP = CLS ? PG_CLS : PAIRS;  // staged (d, w_K, w_D) entries
   if (CLS) {  // class blk * PG_CLS + (t & 15): weights = its chunk partials, added in chunk order
@@ -487,7 +488,7 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
     const int c = q0 + ql;
     double accf = 0.0, accl = 0.0, accw = 0.0;
     if (c < q) {
-      const double a = sa[c], om = so[c];
+      const double a = sa[c], om = so[c], oml = sol[c];
       for (int e = g; e < NP; e += 8) {
         const double wk = swk[e], wd = swd[e];
         if (wk == 0.0 && wd == 0.0) continue;
@@ -496,7 +497,7 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
         radial_l<MATERN>(d, a, m0, m1, m2, m0l, m1l, m2l);
         if (COS) {
           double S, C;
-          sincos(om * d, &S, &C);
+          phase_sincos(om, oml, d, S, C);
           const double c0 = C, c1 = -om * S, c2 = -om * om * C;
           const double c0f = -TWO_PI * d * S;
           const double c1f = -TWO_PI * S - TWO_PI * om * d * C;

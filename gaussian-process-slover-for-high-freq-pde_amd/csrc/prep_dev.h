@@ -9,9 +9,11 @@ namespace gpk {
 
 // exp of the params -> axis constants of component c (prep2 semantics, bitwise)
 __device__ __forceinline__ void axis_component(const PrepArgs& P, int axis, int q, int c, double& w,
-                                               double& a, double& om) {
+                                               double& a, double& om, double& oml) {
   const int off = P.off_kp[axis];
-  om = TWO_PI * P.params[off + c];          // freq
+  const double f = P.params[off + c];       // freq
+  om = TWO_PI * f;
+  oml = om_low(f, om);
   a = exp(P.params[off + q + c]);           // log-ls
   w = exp(P.params[off + 2 * q + c]);       // log-w
 }
@@ -33,9 +35,10 @@ __device__ inline void publish_prep(const PrepArgs& P, int q) {
   const int t = threadIdx.x;
   for (int ax = 0; ax < P.naxes; ++ax)
     for (int c = t; c < q; c += blockDim.x) {
-      double w, a, om;
-      axis_component(P, ax, q, c, w, a, om);
+      double w, a, om, oml;
+      axis_component(P, ax, q, c, w, a, om, oml);
       P.kc[ax].om[c] = om;
+      P.kc[ax].oml[c] = oml;
       P.kc[ax].a[c] = a;
       P.kc[ax].w[c] = w;
     }

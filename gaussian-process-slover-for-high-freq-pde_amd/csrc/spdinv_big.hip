@@ -34,6 +34,7 @@
 #include <atomic>
 
 #include "gemm_huge_dev.h"
+#include "gemm_tile_dev.h"
 #include "gpk_internal.h"
 #include "spd_pivot.h"
 #include "gpk_trace.h"
@@ -692,8 +693,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 // ---- 128-wide sweeps: the update on 128x128 tiles (the large GEMM's tile loop) ------------
-// One workgroup per LOWER 128x128 tile (ti >= tj) computes Z_I^T Z_J with gemm_huge_dev.h's
-// product loop (K = the sweep width, 16-deep double-buffered LDS steps, 4x4 MFMA blocks per wave)
+// One workgroup per LOWER 128x128 tile (ti >= tj) computes Z_I^T Z_J with gemm_tile_dev.h's
+// pipelined product loop (K = the sweep width, 16-deep K-steps in two LDS stages, 4x4 MFMA
+// blocks per wave, stores / loads / reads interleaved with the MFMAs)
 // and applies the sweep's epilogue (sign, zero base in the swept row / column).  Diagonal tiles
 // keep both triangles of their 128 block, so every lower 64-tile the panel reads is current.
 // Workgroup 0 of a factor owns the next pivot block's tile (k+1, k+1): it updates it like the
@@ -701,7 +703,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // updated -- no hand-off, no workgroup waits on another.  The last sweep flips the sign and
 // publishes max diag K^{-1}; big_mirror_kernel then fills the upper triangle.
 constexpr int WT = 128;
-constexpr int WIDE_LDS = 2 * 2 * huge::KS * huge::S;  // the product loop's two staging buffers
+// the product loops' staging buffers (whole tiles: gemm_tile_dev.h; quarter tiles: [k][64] rows at
+// gemm_huge_dev.h's stride)
+constexpr int WIDE_LDS = tile::LDS_DOUBLES > 2 * 2 * huge::KS * huge::S ? tile::LDS_DOUBLES : 2 * 2 * huge::KS * huge::S;
 static_assert(WIDE_LDS >= PIVOT_LDS, "the pivot reuses the staging LDS");
 
 // position pos of sweep k's tile list of a factor with T2 128-tiles per dimension, with a next
@@ -832,12 +836,9 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   constexpr int SZ = KS * S;
   double* sA0 = sm;
   double* sB0 = sm + 2 * SZ;
-  Regs R;
   int m, ti, tj, qq;
   if (!tile_at(0, m, ti, tj, qq)) return;
   int j = 0;
-  if (qq < 0)
-    fetch<1, 0>(R, zbuf<2>(b, m, k), b.p[m], zbuf<2>(b, m, k), b.p[m], b.p[m], b.p[m], WT * ti, WT * tj, 0, t);
   for (; qq < 0; ++j) {
     if (probe && !pivot && j < 2) {  // (trace build) round-0/1 phases over every tile workgroup
       TR_LO(SLOT_BIG_R0START + 3 * j);
@@ -854,20 +855,17 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     const int wK = min(WT, p - WT * k);  // sweep width (a multiple of 32)
     const bool inPi = ti == k, inPj = tj == k;
     const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
-    // the workgroup's next tile (its first K-step is fetched under this tile's last one; a
-    // quarter item is fetched after the loop)
+    // the workgroup's next item
     int m2 = 0, ti2 = 0, tj2 = 0, q2 = -1;
     const bool next = tile_at(j + 1, m2, ti2, tj2, q2);
-    const bool more = next && q2 < 0;
-    // The accumulators start at the tile's current values (zero base in the swept blocks;
-    // clamped addresses: rows / columns past p are never stored) and the product is subtracted
-    // (A operand staged negated): no separate base registers.  The base loads are issued right
-    // behind the tile's first K-step operands (already in flight: fetched under the previous
-    // tile), so they overlap that K-step's staging; with two workgroups per CU the other one's
-    // MFMAs run under their HBM latency.
+    // The accumulators start at the tile's current values NEGATED (zero base in the swept blocks;
+    // clamped addresses: rows / columns past p are never stored) and the product is added; the
+    // store negates back: base - Z_I^T Z_J with the rounding of a subtraction (round-to-nearest
+    // commutes with negation), and no separate base registers.  The base loads are issued ahead
+    // of the product loop's first K-step.
     d4 acc[4][4];
     {
-      const double f = (inPi || inPj) ? 0.0 : 1.0;
+      const double f = (inPi || inPj) ? -0.0 : -1.0;
 #pragma unroll
       for (int bx = 0; bx < 4; ++bx)
 #pragma unroll
@@ -879,26 +877,9 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
             acc[bx][by][r] = X[(size_t)row * p + col] * f;
           }
     }
-    // acc -= Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j]) -- gemm_huge_dev.h's
-    // product loop (product_t<1, 0>, A scaled by -1); R holds K-step 0's operands
-    {
-      const int nk = wK / KS;
-      store<1, 0>(R, sA0, sB0, -1.0, t);
-      __syncthreads();
-      for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) {
-          fetch<1, 0>(R, Z, p, Z, p, p, p, i0, j0, (kt + 1) * KS, t);
-        } else if (more) {
-          const double* Z2 = zbuf<2>(b, m2, k);
-          fetch<1, 0>(R, Z2, b.p[m2], Z2, b.p[m2], b.p[m2], b.p[m2], WT * ti2, WT * tj2, 0, t);
-        }
-        mma(sA0 + cur * SZ, sB0 + cur * SZ, wr, wc, lane, acc);
-        if (kt + 1 < nk) store<1, 0>(R, sA0 + (cur ^ 1) * SZ, sB0 + (cur ^ 1) * SZ, -1.0, t);
-        __syncthreads();
-        if (probe && !pivot && j < 2 && kt == 0) TR_HI(SLOT_BIG_R0START + 3 * j + 1);
-      }
-    }
+    // acc += Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j]) -- both
+    // mn-contiguous, staged [k][mn] without a transpose (tile::product<1, 0>)
+    tile::product<1, 0, false, 0>(Z, p, Z, p, wK, p, p, i0, j0, 1.0, sm, t, wr, wc, lane, acc);
     if (probe && !pivot && j < 2) TR_HI(SLOT_BIG_R0START + 3 * j + 2);
     double mx = 0.0;
 #pragma unroll
@@ -910,7 +891,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
           const int row = i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r;
           const int col = j0 + 64 * wc + 16 * by + (lane & 15);
           if (row < p && col < p) {
-            const double v = sgn * acc[bx][by][r];
+            const double v = -sgn * acc[bx][by][r];
             X[(size_t)row * p + col] = v;
             if (LAST && row == col && row < b.n[m]) mx = fmax(mx, v);
           }
@@ -1007,7 +988,9 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
       const double* sB = sB0 + cur * SZ;
 #pragma unroll
       for (int kk = 0; kk < KS / 4; ++kk) {
-        const int kr = 4 * kk + lk;
+        // (tile::product's k order: MFMA kk of a 16-deep step takes k = 8 (kk >> 1) + 2 lk + (kk & 1)
+        // in k-slot lk, so every output block sees the whole-tile MFMA sequence: bitwise equal)
+        const int kr = 8 * (kk >> 1) + 2 * lk + (kk & 1);
         double a[2], bb[2];
 #pragma unroll
         for (int x = 0; x < 2; ++x) {

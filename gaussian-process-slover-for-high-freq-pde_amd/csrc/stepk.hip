@@ -20,6 +20,7 @@ __global__ void prep2_kernel(const double* __restrict__ params, int off0, int of
     const int off = ax == 0 ? off0 : off1;
     for (int c = t; c < q; c += blockDim.x) {
       kc[ax].om[c] = TWO_PI * params[off + c];      // freq
+      kc[ax].oml[c] = om_low(params[off + c], kc[ax].om[c]);
       kc[ax].a[c] = exp(params[off + q + c]);      // log-ls
       kc[ax].w[c] = exp(params[off + 2 * q + c]);  // log-w
     }

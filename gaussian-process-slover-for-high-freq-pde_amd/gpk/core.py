@@ -226,7 +226,8 @@ class DeviceSolver:
     FIELDS_2D = {"K1": 0, "K2": 1, "K1inv_U": 2, "K2inv_Ut": 3, "U_xx": 4, "U_yy": 5,
                  "G_K1": 6, "G_D1": 7, "G_K2": 8, "G_D2": 9, "K1inv": 10, "K2inv": 11,
                  "K1inv_D1t": 12, "K2inv_D2t": 13, "R": 14, "X1": 15, "X2": 16, "S": 17,
-                 "Kc1": 18, "Kc2": 19, "D1": 20, "D2": 21}
+                 "Kc1": 18, "Kc2": 19, "D1": 20, "D2": 21,
+                 "K1_classes": 22, "K2_classes": 23, "D1_classes": 24, "D2_classes": 25}
     FIELDS_1D = {"K": 0, "Kinv_u": 2, "u_xx": 4, "Kc": 6, "D": 7}
 
     def forward_field(self, name):
@@ -238,6 +239,7 @@ class DeviceSolver:
                      (self.n1, self.n1), (self.n1, self.n1), (self.n2, self.n2), (self.n2, self.n2),
                      (self.n1, self.n1), (self.n2, self.n2), (self.n1, self.n1), (self.n2, self.n2),
                      (self.n1, self.n2), (self.n1, self.n2), (self.n1, self.n2), (self.n1, self.n2),
+                     (self.n1, self.n1), (self.n2, self.n2), (self.n1, self.n1), (self.n2, self.n2),
                      (self.n1, self.n1), (self.n2, self.n2), (self.n1, self.n1), (self.n2, self.n2)][what]
         else:
             what = self.FIELDS_1D[name]

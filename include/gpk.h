@@ -249,7 +249,9 @@ int gpk_criterion(gpk_handle* h, double* out);
  *       12 K1^{-1} D1^T [n1*n1], 13 K2^{-1} D2^T [n2*n2] (augmented chain path only), 14 R,
  *       15 X1, 16 X2, 17 S [n1*n2] (model_GP_solver_2d.py:133 residual),
  *       18 Kc1, 19 Kc2 (the step's kept copy of K, refinement residuals), 20 D1, 21 D2 (the
- *       step's derivative blocks) -- the matrices as the last step assembled them
+ *       step's derivative blocks) -- the matrices as the last step assembled them; 22 K1,
+ *       23 K2, 24 D1, 25 D2 expanded on the host from the distance-class table (class ids +
+ *       class values; handles with classes), the gathers' reference
  *   1D: 0 K [n*n], 2 Kinv_u [n], 4 u_xx [n]; 6 K, 7 D [n*n] as the last step assembled them                                                */
 int gpk_forward_field(gpk_handle* h, int32_t what, double* out, int64_t n);
 

@@ -180,6 +180,8 @@ def kernel_block(kind, x1, x2, paras, deriv=0):
 
 def kernel_kd(kind, x, paras, jitter, deriv):
     """(K + jitter I, D) over the square block of x in one pass (C helper: symmetric, j <= i)."""
+    if _EXTENDED and _EXACT_FIELDS:
+        return kernel_kd_exact(kind, x, paras, jitter, deriv)
     k = _kind_id(kind)
     lib = _clib() if _USE_C else None
     if lib is None:
@@ -205,6 +207,8 @@ def param_grad_contract(kind, x, paras, GK, GD, deriv):
 
     This is what jax.grad pushes through vmap(kappa) / vmap(grad∘grad kappa)
     (code/kernel_matrix.py:26, :49-57). Returns dict of [Q] arrays."""
+    if _EXTENDED and _EXACT_FIELDS:
+        return param_grad_contract_exact(kind, x, paras, GK, GD, deriv)
     k = _kind_id(kind)
     lib = _clib() if _USE_C else None
     if lib is not None:
@@ -261,17 +265,94 @@ def param_grad_contract(kind, x, paras, GK, GD, deriv):
 
 
 # ----------------------------------------------------------------------------------------
+# Exact kernel fields [ext]: the same formulas (kernel_block / param_grad_contract above, the
+# reference's code/kernel_matrix.py:114-193 and its jax.grad contraction) evaluated in long
+# double, with the reference's fp64 inputs and constants (x, exp(log-ls), exp(log-w), freq,
+# 2*pi, sqrt 5).  fp64 evaluation rounds the phase 2*pi*f*d (up to ~250 rad at C5) and the
+# radial argument, which moves cos / sin by ~|phase| * eps -- hundreds of ulp -- and the
+# contraction sum_ij G_ij dK_ij/dtheta cancels those errors into ~1e-8 relative at C5
+# (tools/c5_kp_split.py); an fp64 yardstick shares them with the fp64 LU oracle.
+# One evaluation per distinct pair distance |x_i - x_j| (grids repeat them: ~n variants).
+# ----------------------------------------------------------------------------------------
+def _distance_classes(x):
+    x = np.asarray(x, np.float64).reshape(-1)
+    diff = x[:, None] - x[None, :]
+    du, inv = np.unique(np.abs(diff).ravel(), return_inverse=True)
+    s = np.where(diff >= 0.0, 1.0, -1.0)
+    return du, inv.reshape(diff.shape), s
+
+
+def _exact_field_terms(kind, du, paras):
+    ld = np.longdouble
+    k = _kind_id(kind)
+    a = np.exp(np.asarray(paras["log-ls"], np.float64)).astype(ld)
+    f = np.asarray(paras["freq"], np.float64).astype(ld)
+    dd = du.astype(ld)[:, None]
+    rad = _radial(k, dd, a, True)
+    cos = _cosine(k, dd, f, True)
+    return k, rad, cos
+
+
+def kernel_kd_exact(kind, x, paras, jitter, deriv):
+    """kernel_kd with the fields evaluated exactly (long double), then rounded to fp64."""
+    du, inv, s = _distance_classes(x)
+    k, (m0, m1, m2, _, _, _), (c0, c1, c2, _, _, _) = _exact_field_terms(kind, du, paras)
+    w = np.exp(np.asarray(paras["log-w"], np.float64)).astype(np.longdouble)
+    Ku = ((m0 * c0) @ w).astype(np.float64)
+    if deriv == 2:
+        Du = ((m2 * c0 + 2.0 * m1 * c1 + m0 * c2) @ w).astype(np.float64)
+    else:
+        Du = ((m1 * c0 + m0 * c1) @ w).astype(np.float64)
+    K = Ku[inv]
+    K[np.diag_indices_from(K)] += jitter
+    D = Du[inv] * s if deriv == 1 else Du[inv]
+    return K, D
+
+
+def param_grad_contract_exact(kind, x, paras, GK, GD, deriv):
+    """param_grad_contract exactly: G summed per distance class in long double, contracted with
+    the long-double derivative fields, rounded once at the end."""
+    ld = np.longdouble
+    du, inv, s = _distance_classes(x)
+    flat = inv.ravel()
+    order = np.argsort(flat, kind="stable")
+    starts = np.searchsorted(flat[order], np.arange(du.size))
+    SK = np.add.reduceat(np.asarray(GK, np.float64).ravel()[order].astype(ld), starts)
+    k, (m0, m1, m2, m0l, m1l, m2l), (c0, c1, c2, c0f, c1f, c2f) = _exact_field_terms(kind, du, paras)
+    gw, gl, gf = SK @ (m0 * c0), SK @ (m0l * c0), SK @ (m0 * c0f)
+    if GD is not None:
+        g = np.asarray(GD, np.float64) * (s if deriv == 1 else 1.0)
+        SD = np.add.reduceat(g.ravel()[order].astype(ld), starts)
+        if deriv == 2:
+            Dw = m2 * c0 + 2.0 * m1 * c1 + m0 * c2
+            Dl = m2l * c0 + 2.0 * m1l * c1 + m0l * c2
+            Df = m2 * c0f + 2.0 * m1 * c1f + m0 * c2f
+        else:
+            Dw, Dl, Df = m1 * c0 + m0 * c1, m1l * c0 + m0l * c1, m1 * c0f + m0 * c1f
+        gw, gl, gf = gw + SD @ Dw, gl + SD @ Dl, gf + SD @ Df
+    w = np.exp(np.asarray(paras["log-w"], np.float64)).astype(ld)
+    out = {"freq": gf * w, "log-ls": gl * w, "log-w": gw * w}
+    if not _has_cos(k):
+        out["freq"] = out["freq"] * 0
+    return {n: v.astype(np.float64) for n, v in out.items()}
+
+
+# ----------------------------------------------------------------------------------------
 # LU helpers mirroring jnp.linalg.solve / slogdet (LAPACK getrf + getrs) [ext]
 # ----------------------------------------------------------------------------------------
 _EXTENDED = False
+_EXACT_FIELDS = True
 
 
-def set_extended(flag):
-    """Extended-precision mode (x87 80-bit long double LU) for the solves / inverses / log-det:
-    an 'exact arithmetic' yardstick (eps 5.4e-20) for sizing the parity tolerances of
-    ill-conditioned cases.  Kernel fields and contractions stay fp64."""
-    global _EXTENDED
+def set_extended(flag, exact_fields=True):
+    """Extended-precision mode: the 'exact arithmetic' yardstick for sizing the parity
+    tolerances of ill-conditioned cases.  Solves / inverses / log-det in x87 80-bit long double
+    LU (eps 5.4e-20), and -- unless exact_fields=False (the round-4 yardstick) -- the kernel
+    fields K, D and the kernel-parameter contraction exact too (kernel_kd_exact,
+    param_grad_contract_exact).  The remaining products (residual, G assembly) stay fp64."""
+    global _EXTENDED, _EXACT_FIELDS
     _EXTENDED = bool(flag)
+    _EXACT_FIELDS = bool(exact_fields)
 
 
 _EXTLIB = None

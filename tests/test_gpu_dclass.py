@@ -101,3 +101,23 @@ def test_c4_size_class_counts():
     assert s.class_counts() == [1297, 1297]
     s.close()
 
+
+
+@pytest.mark.parametrize("eq,n1,n2", [("advection", 1056, 64), ("poisson", 1024, 1056)])
+def test_wide_gather_bitwise_class_table(eq, n1, n2):
+    """The large-factor gather (p >= 1024: gather_wide_kernel, class = cbase[|i - j|] + the pair's
+    variant byte) writes exactly the class table's values: K (+ jitter), its kept copy and D
+    (with the advection sign) bitwise equal to the host expansion of (class ids, class values)."""
+    prob, params, _, fs = problem_2d(eq=eq, kind="Matern52_Cos_1d", n1=n1, n2=n2, Q=4, seed=5)
+    s = device_solver(prob, 4, fs)
+    try:
+        s.set_params(params)
+        s.loss_grad()
+        for a in (1, 2):
+            n = n1 if a == 1 else n2
+            if n < 1024:
+                continue
+            assert np.array_equal(s.forward_field(f"Kc{a}"), s.forward_field(f"K{a}_classes"))
+            assert np.array_equal(s.forward_field(f"D{a}"), s.forward_field(f"D{a}_classes"))
+    finally:
+        s.close()

@@ -10,7 +10,13 @@ contraction is linear, so kernel_paras_2's error splits exactly into
   gd     : G_D2_dev - G_D2_ext
 each reported as max-abs / max-abs of the yardstick's kernel_paras_2 (tests/helpers.rel), next to
 the same split of the fp64 LU oracle (the reference algorithm) on the same K and D.
-usage: python tools/c5_kp_split.py [C5] [--axis 2]"""
+
+"contraction" separates the contraction's own rounding from the G matrices': each G is contracted
+exactly (class sums over the distinct pair distances and the derivative fields in long double, the
+reference's fp64 constants and exp(log-ls)), and the device gradient, the fp64 oracle contraction
+(oracle/gp_oracle.py param_grad_contract) and the yardstick's own fp64 contraction are each
+measured against the exact contraction of the G they contracted.
+usage: python tools/c5_kp_split.py [C5] [2]"""
 import argparse
 import json
 import os
@@ -25,10 +31,47 @@ from tests.helpers import config_problem
 import tools.solve_accuracy as SA
 
 
+def contract_ld(kind, x, kp, GK, GD, deriv, sums64=False, fields64=False):
+    """Exact (long-double) contraction of GK, GD with the derivative fields of kernel kind
+    (oracle/gp_oracle.py param_grad_contract's formulas), summed per distinct pair distance."""
+    k = O._kind_id(kind)
+    x = np.asarray(x, np.float64)
+    diff = x[:, None] - x[None, :]
+    d = np.abs(diff).ravel()
+    du, inv = np.unique(d, return_inverse=True)
+    order = np.argsort(inv, kind="stable")
+    starts = np.searchsorted(inv[order], np.arange(du.size))
+    ld = np.longdouble
+    sdt = np.float64 if sums64 else ld  # sums64 / fields64: that half in fp64 (diagnostics)
+    SK = np.add.reduceat(GK.ravel()[order].astype(sdt), starts).astype(ld)
+    SD = None
+    if GD is not None:
+        g = GD.ravel() * (np.where(diff >= 0.0, 1.0, -1.0).ravel() if deriv == 1 else 1.0)
+        SD = np.add.reduceat(g[order].astype(sdt), starts).astype(ld)
+    fdt = np.float64 if fields64 else ld
+    w = np.exp(np.asarray(kp["log-w"], np.float64)).astype(ld)
+    a = np.exp(np.asarray(kp["log-ls"], np.float64)).astype(fdt)
+    f = np.asarray(kp["freq"], np.float64).astype(fdt)
+    dd = du.astype(fdt)[:, None]
+    m0, m1, m2, m0l, m1l, m2l = (v.astype(ld) for v in O._radial(k, dd, a, True))
+    c0, c1, c2, c0f, c1f, c2f = (np.asarray(v).astype(ld) for v in O._cosine(k, dd, f, True))
+    gw, gl, gf = SK @ (m0 * c0), SK @ (m0l * c0), SK @ (m0 * c0f)
+    if SD is not None:
+        if deriv == 2:
+            Dw, Dl, Df = m2 * c0 + 2 * m1 * c1 + m0 * c2, m2l * c0 + 2 * m1l * c1 + m0l * c2, m2 * c0f + 2 * m1 * c1f + m0 * c2f
+        else:
+            Dw, Dl, Df = m1 * c0 + m0 * c1, m1l * c0 + m0l * c1, m1 * c0f + m0 * c1f
+        gw, gl, gf = gw + SD @ Dw, gl + SD @ Dl, gf + SD @ Df
+    if not O._has_cos(k):
+        gf = gf * 0
+    out = {"freq": gf * w, "log-ls": gl * w, "log-w": gw * w}
+    return np.concatenate([out[n].reshape(-1) for n in sorted(out)])  # _flatten's order, long double
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("config", nargs="?", default="C5")
-    ap.add_argument("--axis", type=int, default=2)
+    ap.add_argument("axis", nargs="?", type=int, default=2)
     a = ap.parse_args()
     from gpk.problems import make_solver
     O.set_backend(True)
@@ -92,6 +135,27 @@ def main():
               "lu_oracle": split(GKl, GDl, Kinv_lu),
               "kinv_rel_err": {"device": float(np.max(np.abs(fld[f"K{ax}inv"] - Kinv_ext)) / np.max(np.abs(Kinv_ext))),
                                "lu": float(np.max(np.abs(Kinv_lu - Kinv_ext)) / np.max(np.abs(Kinv_ext)))}}
+    # the contraction's own rounding, against the exact contraction of the G each one contracted
+    ex_dev = contract_ld(kind, x, kp, fld[f"G_K{ax}"], fld[f"G_D{ax}"], deriv)
+    ex_ext = contract_ld(kind, x, kp, GKx, GDx, deriv)
+    ex_lu = contract_ld(kind, x, kp, GKl, GDl, deriv)
+    print("exact contractions done", flush=True)
+
+    def e(v, ref):
+        return float(np.max(np.abs(np.asarray(v, np.longdouble) - ref))) / scale
+    report["contraction"] = {
+        "device_step_vs_exact_of_device_G": e(O.flatten_params(dev_g[key]), ex_dev),
+        "oracle_fp64_vs_exact_of_device_G": e(contract(fld[f"G_K{ax}"], fld[f"G_D{ax}"]), ex_dev),
+        "yardstick_fp64_vs_exact_of_its_G": e(gref, ex_ext),
+        "lu_fp64_vs_exact_of_its_G": e(res["lu"][1][key], ex_lu),
+        "exact_device_G_vs_exact_yardstick_G": e(ex_dev, ex_ext),
+        "exact_lu_G_vs_exact_yardstick_G": e(ex_lu, ex_ext),
+        "device_step_vs_exact_yardstick_G": e(O.flatten_params(dev_g[key]), ex_ext),
+        "lu_fp64_vs_exact_yardstick_G": e(res["lu"][1][key], ex_ext),
+        # which half of an fp64 contraction carries the rounding: fp64 class sums (sequential per
+        # distance) with exact fields, and exact sums with fp64 fields
+        "fp64_sums_exact_fields_of_device_G": e(contract_ld(kind, x, kp, fld[f"G_K{ax}"], fld[f"G_D{ax}"], deriv, sums64=True), ex_dev),
+        "exact_sums_fp64_fields_of_device_G": e(contract_ld(kind, x, kp, fld[f"G_K{ax}"], fld[f"G_D{ax}"], deriv, fields64=True), ex_dev)}
     print(json.dumps(report, indent=1), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out", "r5"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "r5", f"kp_split_{a.config}_{ax}.json"), "w") as f:

@@ -6,7 +6,9 @@ the raw value is kept too because our loads are 8-B-per-lane (uncalibrated width
 from the L2 memory side and include Infinity-Cache hits, so at working sets < 256 MiB they are an
 upper bound on DRAM bytes.
 
-usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>
+usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json> [tree]
+(tree: the source tree the passes measured, e.g. its git head -- recorded in the summary so the
+bench line's roofline.traffic names what it was measured on)
 """
 import collections
 import csv
@@ -30,6 +32,7 @@ def per_kernel(d, counter):
 
 def main():
     fetch, write, out = sys.argv[1:4]
+    tree = sys.argv[4] if len(sys.argv) > 4 else None
     fr, wr = per_kernel(fetch, "FETCH_SIZE"), per_kernel(write, "WRITE_SIZE")
     res = {}
     for k in sorted(set(fr) | set(wr)):
@@ -40,7 +43,7 @@ def main():
     with open(out, "w") as f:
         json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) "
                              "of bench.py; traffic_bytes = 2*FETCH + WRITE per launch",
-                   "kernels": res}, f, indent=1)
+                   "tree": tree, "kernels": res}, f, indent=1)
     for k, v in res.items():
         print(f"{k:40s} fetch {v['fetch_bytes_x2'] / 1e6:9.3f} MB  write {v['write_bytes'] / 1e6:9.3f} MB")
 

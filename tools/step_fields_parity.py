@@ -27,8 +27,7 @@ from oracle import gp_oracle as O
 from tests.helpers import config_problem
 import tools.solve_accuracy as SA
 
-FLOOR = {"C1": 1e-10, "C2": 1e-8, "C3": 1e-10, "C4": 1e-10, "C5": 1e-8}
-MULT = {"C1": 4.0, "C2": 4.0, "C3": 4.0, "C4": 4.0, "C5": 1.0}
+from tests.test_gpu_accuracy import FLOOR, MULT  # noqa: E402  (the same bars)
 
 
 def main():
