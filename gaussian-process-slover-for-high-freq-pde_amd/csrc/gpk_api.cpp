@@ -120,6 +120,8 @@ struct gpk_handle {
   double *red_quad = nullptr, *red_egap = nullptr;
   int nquad = 0, negap = 0;
   double *pgpart = nullptr, *pg = nullptr;
+  double *pgpart_lo = nullptr, *tgpart_lo = nullptr;  // DD contraction (pg_dd): low parts
+  bool pg_dd = false;                 // kernel-parameter contraction in double-double
   int bpa = 0;
   // fused step tail (pgrad launch): group counters / partials, boundary gap
   unsigned int *tcount = nullptr, *ttop = nullptr;
@@ -404,6 +406,7 @@ static TailArgs make_tail(gpk_handle* h, int apply, bool refine = true) {
   else { au.S = nullptr; au.X1 = h->alpha; au.X2 = h->beta; au.R = h->R; au.U0 = h->uoff; }
   T.gcount = h->tcount; T.top = h->ttop; T.gpart = h->tgpart; T.pg = h->pg;
   T.tg = h->ttg; T.ngpa = h->tngpa;
+  T.gpart_lo = h->pg_dd ? h->tgpart_lo : nullptr;
   return T;
 }
 
@@ -458,6 +461,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
       pa[a].GD = h->GD[a];
       pa[a].deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
+      pa[a].part_lo = h->pg_dd ? h->pgpart_lo + (size_t)a * h->bpa * 3 * QMAX : nullptr;
       pa[a].cls = h->cls[a];
     }
     TailArgs tail = make_tail(h, apply, refine);
@@ -1606,6 +1610,15 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   A_(h->tcount, (size_t)L.naxes * h->tngpa);
   A_(h->ttop, 1);
   A_(h->tgpart, (size_t)L.naxes * h->tngpa * 3 * QMAX);
+  // The kernel-parameter contraction in double-double on the large 2D factors (C5): there the
+  // sum over classes cancels ~1e8-fold and the fp64 rounding of the derivative fields sets its
+  // accuracy; at C4 it would cost the latency-bound step ~1 us and buys nothing
+  h->pg_dd = use_cls && L.dim == 2 && !shard && !(p->flags & GPK_FLAG_NO_DD_CONTRACTION) &&
+             (std::max(P1, P2) >= SPD_WIDE_MIN || (p->flags & GPK_FLAG_DD_CONTRACTION));
+  if (h->pg_dd) {
+    A_(h->pgpart_lo, (size_t)L.naxes * h->bpa * 3 * QMAX);
+    A_(h->tgpart_lo, (size_t)L.naxes * h->tngpa * 3 * QMAX);
+  }
   A_(h->bgap, 1);
   A_(h->snap, (size_t)3 * L.nparams);
   A_(h->snap_count, 1);

@@ -417,6 +417,9 @@ struct PGradArgs {
   double halfc;                           // 1D mode: 0.5*logdet flag
   int deriv;
   double* part;                           // [nblocks * 3*QMAX]
+  // DD (class path, 2D, fused tail): the derivative fields and every sum after them in
+  // double-double; part holds the partials' high parts, part_lo their low parts (null: fp64)
+  double* part_lo;
   ClassArgs cls;                          // ncls > 0: class sums + per-class contraction
 };
 struct TailArgs;  // stepk.h

@@ -19,6 +19,7 @@
 
 #include "gpk_internal.h"
 #include "gpk_trace.h"
+#include "fields_dd.h"
 
 namespace gpk {
 GPK_TRACE_TU(pgrad)
@@ -102,6 +103,24 @@ __device__ __forceinline__ double strided_sum(const double* p, int stride, int n
   return acc;
 }
 
+// the same sum of double-double values (high parts at ph, low parts at pl), in index order
+__device__ __forceinline__ dd::D strided_sum_dd(const double* ph, const double* pl, int stride, int n) {
+  dd::D acc = {0.0, 0.0};
+  for (int k = 0; k < n; k += 16) {
+    double vh[16], vl[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const size_t o = (size_t)(k + j < n ? k + j : k) * stride;
+      vh[j] = ld_wt(ph + o);
+      vl[j] = ld_wt(pl + o);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (k + j < n) acc = dd::add(acc, dd::D{vh[j], vl[j]});
+  }
+  return acc;
+}
+
 __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
   const TailArgs& T = b.tail;
   __shared__ int s_last;
@@ -116,11 +135,22 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
     TR_HI(SLOT_PG_GARR);
   }
   const double* part = b.ax[axis].part;
+  const double* part_lo = b.ax[axis].part_lo;
   for (int x = t; x < 3 * QMAX; x += 256) {
+    const size_t go = (size_t)(axis * T.ngpa + gi) * (3 * QMAX) + x;
+    if (T.gpart_lo) {  // DD: the group's partials summed in double-double
+      dd::D acc = {0.0, 0.0};
+      if ((x % QMAX) < q)
+        acc = strided_sum_dd(part + (size_t)gi * T.tg * (3 * QMAX) + x,
+                             part_lo + (size_t)gi * T.tg * (3 * QMAX) + x, 3 * QMAX, gsize);
+      st_wt(T.gpart + go, acc.h);
+      st_wt(T.gpart_lo + go, acc.l);
+      continue;
+    }
     double acc = 0.0;
     if ((x % QMAX) < q)
       acc = strided_sum(part + (size_t)gi * T.tg * (3 * QMAX) + x, 3 * QMAX, gsize);
-    st_wt(T.gpart + (size_t)(axis * T.ngpa + gi) * (3 * QMAX) + x, acc);
+    st_wt(T.gpart + go, acc);
   }
   if (t == 0) T.gcount[axis * T.ngpa + gi] = 0u;  // re-arm (no other user this step)
   if (t == 0) TR_HI(SLOT_PG_GROUP);
@@ -131,7 +161,13 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
   for (int e = t; e < b.naxes * 3 * q; e += 256) {
     const int ax = e / (3 * q), rem = e % (3 * q);
     const int x = (rem / q) * QMAX + rem % q;
-    T.pg[ax * 3 * QMAX + x] = strided_sum(T.gpart + (size_t)ax * T.ngpa * (3 * QMAX) + x, 3 * QMAX, T.ngpa);
+    if (T.gpart_lo) {
+      const dd::D acc = strided_sum_dd(T.gpart + (size_t)ax * T.ngpa * (3 * QMAX) + x,
+                                       T.gpart_lo + (size_t)ax * T.ngpa * (3 * QMAX) + x, 3 * QMAX, T.ngpa);
+      T.pg[ax * 3 * QMAX + x] = acc.h + acc.l;
+    } else {
+      T.pg[ax * 3 * QMAX + x] = strided_sum(T.gpart + (size_t)ax * T.ngpa * (3 * QMAX) + x, 3 * QMAX, T.ngpa);
+    }
   }
   __syncthreads();  // pg (global) written by this block is visible to it after the barrier
   if (t == 0) *T.top = 0u;
@@ -369,7 +405,7 @@ __global__ __launch_bounds__(256) void class_sum_kernel(PGradBatch b,
 
 constexpr int PG_CLS = 16;  // classes per contraction workgroup
 
-template <bool MATERN, bool COS, int DERIV, bool MODE1D, bool CLS>
+template <bool MATERN, bool COS, int DERIV, bool MODE1D, bool CLS, bool DD = false>
 __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
                                                     const StepScalars* __restrict__ sc) {
   const int axis = blockIdx.y;
@@ -484,15 +520,25 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
 
   const int g = t >> 5, ql = t & 31;
   double* out = A.part + (size_t)blk * (3 * QMAX);
+  __shared__ double slo[DD ? 8 : 1][3][32];  // DD: the low parts of sacc
   for (int q0 = 0; q0 < q; q0 += 32) {
     const int c = q0 + ql;
     double accf = 0.0, accl = 0.0, accw = 0.0;
+    dd::D xf = {0.0, 0.0}, xl = {0.0, 0.0}, xw = {0.0, 0.0};
     if (c < q) {
       const double a = sa[c], om = so[c], oml = sol[c];
       for (int e = g; e < NP; e += 8) {
         const double wk = swk[e], wd = swd[e];
         if (wk == 0.0 && wd == 0.0) continue;
         const double d = sd[e];
+        if constexpr (DD) {
+          dd::D fw, fl, ff, dw, dl, df;
+          fields_dd<MATERN, COS, DERIV>(d, a, om, oml, fw, fl, ff, dw, dl, df);
+          xw = dd::add(xw, dd::add(dd::mul_d(fw, wk), dd::mul_d(dw, wd)));
+          xl = dd::add(xl, dd::add(dd::mul_d(fl, wk), dd::mul_d(dl, wd)));
+          xf = dd::add(xf, dd::add(dd::mul_d(ff, wk), dd::mul_d(df, wd)));
+          continue;
+        }
         double m0, m1, m2, m0l, m1l, m2l;
         radial_l<MATERN>(d, a, m0, m1, m2, m0l, m1l, m2l);
         if (COS) {
@@ -523,18 +569,37 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
         }
       }
     }
-    sacc[g][0][ql] = accf;
-    sacc[g][1][ql] = accl;
-    sacc[g][2][ql] = accw;
+    if constexpr (DD) {
+      sacc[g][0][ql] = xf.h;
+      sacc[g][1][ql] = xl.h;
+      sacc[g][2][ql] = xw.h;
+      slo[g][0][ql] = xf.l;
+      slo[g][1][ql] = xl.l;
+      slo[g][2][ql] = xw.l;
+    } else {
+      sacc[g][0][ql] = accf;
+      sacc[g][1][ql] = accl;
+      sacc[g][2][ql] = accw;
+    }
     __syncthreads();
     if (t < 96) {
       const int which = t >> 5, qq = t & 31;
-      double s = 0.0;
+      if constexpr (DD) {  // (only with the fused tail: launch_pg_c)
+        dd::D s = {0.0, 0.0};
 #pragma unroll
-      for (int gg = 0; gg < 8; ++gg) s += sacc[gg][which][qq];
-      if (q0 + qq < QMAX) {
-        if (b.tail.fused) st_wt(out + which * QMAX + q0 + qq, s);  // write-through: handed off
-        else out[which * QMAX + q0 + qq] = s;
+        for (int gg = 0; gg < 8; ++gg) s = dd::add(s, dd::D{sacc[gg][which][qq], slo[gg][which][qq]});
+        if (q0 + qq < QMAX) {
+          st_wt(out + which * QMAX + q0 + qq, s.h);
+          st_wt(A.part_lo + (size_t)blk * (3 * QMAX) + which * QMAX + q0 + qq, s.l);
+        }
+      } else {
+        double s = 0.0;
+#pragma unroll
+        for (int gg = 0; gg < 8; ++gg) s += sacc[gg][which][qq];
+        if (q0 + qq < QMAX) {
+          if (b.tail.fused) st_wt(out + which * QMAX + q0 + qq, s);  // write-through: handed off
+          else out[which * QMAX + q0 + qq] = s;
+        }
       }
     }
     __syncthreads();
@@ -580,6 +645,16 @@ static void launch_pg_c(const PGradBatch& b, int naxes, int bpa, int q, int deri
   // the U plane (dL/dU + Adam) gets one element per thread when it is wider than bpa blocks
   const int ublocks = b.tail.fused ? (tail_nu(b.tail.adam.L) + 255) / 256 : 0;
   dim3 grid(std::max(bpa, std::min(ublocks, 4096)), naxes + (b.tail.fused ? 2 : 0));
+  // double-double contraction: class path, 2D, with the fused tail carrying the low parts
+  const bool ddc = CLS && !mode1d && b.tail.fused && b.tail.gpart_lo && b.ax[0].part_lo &&
+                   (naxes < 2 || b.ax[1].part_lo);
+  if (ddc) {
+    if (deriv == 2)
+      hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, false, CLS, true>), grid, dim3(256), 0, s, b, q, sc);
+    else
+      hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 1, false, CLS, true>), grid, dim3(256), 0, s, b, q, sc);
+    return;
+  }
   if (mode1d) {
     hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, true, CLS>), grid, dim3(256), 0, s, b, q, sc);
   } else if (deriv == 2) {

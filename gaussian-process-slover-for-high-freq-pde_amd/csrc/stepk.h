@@ -91,6 +91,7 @@ struct TailArgs {
   double* gpart;             // [naxes * ngpa][3*QMAX] group partials
   double* pg;                // [naxes][3*QMAX] reduced parameter gradients (-> fin.pg)
   int tg, ngpa;              // blocks per group, groups per axis
+  double* gpart_lo;          // DD contraction: the group partials' low parts (null: fp64)
 };
 
 hipError_t launch_step_begin(const StepBegin& b, hipStream_t s);

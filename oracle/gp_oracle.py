@@ -282,14 +282,45 @@ def _distance_classes(x):
     return du, inv.reshape(diff.shape), s
 
 
+def _two_prod(a, b):
+    """Dekker's error-free product in fp64 (Veltkamp splits, no FMA): a*b = p + e exactly."""
+    p = a * b
+    c = 134217729.0 * a
+    ah = c - (c - a)
+    al = a - ah
+    c = 134217729.0 * b
+    bh = c - (c - b)
+    bl = b - bh
+    return p, ((ah * bh - p) + ah * bl + al * bh) + al * bl
+
+
 def _exact_field_terms(kind, du, paras):
     ld = np.longdouble
     k = _kind_id(kind)
     a = np.exp(np.asarray(paras["log-ls"], np.float64)).astype(ld)
-    f = np.asarray(paras["freq"], np.float64).astype(ld)
+    f64 = np.asarray(paras["freq"], np.float64)
+    f = f64.astype(ld)
     dd = du.astype(ld)[:, None]
     rad = _radial(k, dd, a, True)
     cos = _cosine(k, dd, f, True)
+    if _has_cos(k):
+        # the phase 2 pi f d exactly: a long double holds it only to ~1.4e-17 absolute at C5's
+        # ~250 rad (as much as 1/8 of fp64's own field rounding, amplified ~1e8 by the
+        # contraction), so it is carried as phi_h + phi_l (error-free products in fp64) and
+        # cos / sin are taken at the exactly representable phi_h, corrected to first order
+        wh, wl = _two_prod(TWO_PI, f64)                            # 2 pi f = wh + wl
+        d64 = np.asarray(du, np.float64)[:, None]
+        ph, e1 = _two_prod(wh[None, :], d64)
+        pl = e1.astype(ld) + wl.astype(ld)[None, :] * d64.astype(ld)  # phase = ph + pl
+        Ch, Sh = np.cos(ph.astype(ld)), np.sin(ph.astype(ld))
+        C = Ch - pl * Sh
+        S = Sh + pl * Ch
+        w = wh.astype(ld) + wl.astype(ld)
+        c0, c1, c2 = C, -w * S, -w * w * C
+        c0f = -TWO_PI * dd * S
+        c1f = -TWO_PI * S - TWO_PI * w * dd * C
+        c2f = -4.0 * math.pi * w * C + TWO_PI * w * w * dd * S
+        cos = (c0, c1, c2, c0f, c1f, c2f)
     return k, rad, cos
 
 
