@@ -229,5 +229,64 @@ __device__ __forceinline__ void product(const double* A, int lda, const double* 
   __syncthreads();  // the LDS is reused (a second product, the epilogue's partial sums)
 }
 
+// acc += sa1 op(A1) op(B1) [K1] + sa2 op(A2) op(B2) [K2]: product's pipeline over the two
+// sources back to back (one prologue and one drain for K1 + K2; the C5 SPD inverse's two-sweep
+// tile updates).  A1 / A2 (B1 / B2) share lda (ldb); both K are multiples of 32.
+template <int ta, int tb>
+__device__ __forceinline__ void product2(const double* A1, const double* B1, int K1, double sa1,
+                                         const double* A2, const double* B2, int K2, double sa2,
+                                         int lda, int ldb, int M, int N, int i0, int j0, double* lds,
+                                         int t, int wr, int wc, int lane, d4 (&acc)[4][4]) {
+  using C = Counts<ta, tb>;
+  const int nk1 = K1 / KS, nk = nk1 + K2 / KS;
+  auto fetch_s = [&](Glob& g, int s) {
+    const bool one = s < nk1;
+    fetch<ta, tb>(g, one ? A1 : A2, lda, one ? B1 : B2, ldb, M, N, i0, j0, (one ? s : s - nk1) * KS, t);
+  };
+  auto put_s = [&](const Glob& g, double* st, int s) { put<ta, tb, true>(g, st, s < nk1 ? sa1 : sa2, t); };
+  Glob g;
+  Frag f0, f1;
+  fetch_s(g, 0);
+  put_s(g, lds, 0);
+  fetch_s(g, 1);
+  __syncthreads();
+  get<ta, tb>(f0, lds, 0, wr, wc, lane);
+  int s = 0;
+  for (; s + 2 < nk; ++s) {
+    double* cur = lds + (s & 1) * STAGE;
+    double* nxt = lds + ((s & 1) ^ 1) * STAGE;
+    put_s(g, nxt, s + 1);
+    fetch_s(g, s + 2);
+    get<ta, tb>(f1, cur, 1, wr, wc, lane);
+    mma(f0, acc);
+    interleave<C::writes, C::loads, C::reads>();
+    __syncthreads();
+    get<ta, tb>(f0, nxt, 0, wr, wc, lane);
+    mma(f1, acc);
+    interleave<0, 0, C::reads>();
+  }
+  {
+    double* cur = lds + (s & 1) * STAGE;
+    double* nxt = lds + ((s & 1) ^ 1) * STAGE;
+    put_s(g, nxt, s + 1);
+    get<ta, tb>(f1, cur, 1, wr, wc, lane);
+    mma(f0, acc);
+    interleave<C::writes, 0, C::reads>();
+    __syncthreads();
+    get<ta, tb>(f0, nxt, 0, wr, wc, lane);
+    mma(f1, acc);
+    interleave<0, 0, C::reads>();
+    ++s;
+  }
+  {
+    double* cur = lds + (s & 1) * STAGE;
+    get<ta, tb>(f1, cur, 1, wr, wc, lane);
+    mma(f0, acc);
+    interleave<0, 0, C::reads>();
+    mma(f1, acc);
+  }
+  __syncthreads();
+}
+
 }  // namespace tile
 }  // namespace gpk

@@ -138,7 +138,8 @@ struct gpk_handle {
   // large 1D factors with distance classes: the GEMVs read Kc and D as class ids + class values
   // (GemvDesc::cid), so the inverse launch's gather writes neither matrix (64 MB at C2)
   bool cls_gemv = false;
-  double* Zp[2] = {};                 // ... its double-buffered panel [2][128][P]
+  double* Zp[2] = {};                 // ... its panel buffers [3][128][P] (by sweep mod 3)
+  unsigned* wsched[2] = {};           // ... its two-sweep update schedule (wide_schedule)
   bool chain = false;                 // small factors: persistent one-launch inverse (chain_kernel)
   bool chain_aug = false;             // ... which also solves A, Bt^T and K^{-1} D^T (2D, unsharded)
   unsigned int* cflags[2] = {};       // its hand-off flags [T*(T+taug) + 2T + 1] per factor
@@ -262,6 +263,7 @@ static void fill_spd(gpk_handle* h, SpdArgs* sa) {
     sa[a].wide = h->bigwide ? 1 : 0;
     sa[a].no_quarters = (h->prob.flags & GPK_FLAG_NO_QUARTER_TILES) ? 1 : 0;
     sa[a].Z = h->Zp[a];
+    sa[a].sched = h->wsched[a];
   }
 }
 
@@ -1518,7 +1520,16 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     A_(h->Kc[a], (size_t)P * P);
     A_(h->pst[a], 2);
     A_(h->aflag[a], 4 + P / 32);  // + the 128-wide update's per-sweep panel tickets
-    if (h->bigspd) A_(h->Zp[a], (size_t)2 * 128 * P);
+    if (h->bigspd) A_(h->Zp[a], (size_t)3 * 128 * P);
+    if (h->bigspd && h->bigwide && !(p->flags & GPK_FLAG_ONE_SWEEP_UPDATE)) {
+      const int T2 = (int)((P + 127) / 128);
+      std::vector<unsigned> tab;
+      wide_schedule(T2, true, tab);
+      A_(h->wsched[a], tab.size());
+      if (hipMemcpyAsync(h->wsched[a], tab.data(), tab.size() * sizeof(unsigned), hipMemcpyHostToDevice, h->s) != hipSuccess ||
+          hipStreamSynchronize(h->s) != hipSuccess)
+        return bail(fail(GPK_EHIP, "upload the update schedule"));
+    }
     A_(h->cflags[a], (size_t)(P / 32) * (P / 32 + (P1 + P2) / 32) + 2 * (P / 32) + 1);
     A_(h->cgran[a], (size_t)(P / 32) * 2048);
     // every hand-off slot starts unwritten (spdinv.hip chain_master / chain_multi_kernel)
@@ -2900,6 +2911,15 @@ int gpk_dgemm(int32_t variant, int32_t M, int32_t N, int32_t K, double alpha, co
 }
 
 }  // extern "C"
+
+int gpk_wide_schedule(int32_t T2, int32_t paired, uint32_t* out, int64_t cap) {
+  if (T2 < 1 || T2 > 255 || !out) return fail(GPK_EINVAL, "gpk_wide_schedule: T2 in [1, 255], out non-null");
+  std::vector<unsigned> tab;
+  wide_schedule(T2, paired != 0, tab);
+  if ((int64_t)tab.size() > cap) return fail(GPK_EINVAL, "gpk_wide_schedule: cap too small");
+  std::memcpy(out, tab.data(), tab.size() * sizeof(unsigned));
+  return GPK_OK;
+}
 
 // error / device helpers for the other C-ABI translation units (gpk_kron3.cpp)
 namespace gpk {

@@ -3,6 +3,7 @@
 // Closed-form spectral-mixture kernel fields replacing the
 // reference's jax.grad-of-kappa machinery (code/kernel_matrix.py:49-57, :114-193).
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -214,8 +215,17 @@ struct SpdArgs {
   unsigned int* flag;  // large path: [3] hand-off / pivot-done / panel-row counters
   int wide;        // large path: 128-wide sweeps (else 64)
   int no_quarters; // 128-wide update: keep the last round in whole tiles (tests, GPK_FLAG_NO_QUARTER_TILES)
-  double* Z;       // large path: double-buffered panel [2][128][p] (nullable: Y)
+  double* Z;       // large path: panel buffers [3][128][p] by sweep mod 3 (nullable: Y)
+  // 128-wide update schedule (wide_schedule): per sweep, the tiles the launch updates and the
+  // sweeps (1 or 2) each applies; null: every tile every sweep (the one-sweep form)
+  const unsigned* sched;
 };
+// Two-sweep schedule of the 128-wide update (spdinv_big.hip): per sweep k of a factor with T2
+// 128-tiles per dimension, row k of tab (stride wide_sched_stride(T2)) holds [0] the tile count,
+// [1] the next pivot tile's entry, [2 + i] tile i's entry: J | I << 8 | two << 16 | c0 << 18 |
+// c1 << 20 | c2 << 22 (codes 0, 1 = +1, 3 = -1).  paired = false: every tile every sweep.
+int wide_sched_stride(int T2);
+void wide_schedule(int T2, bool paired, std::vector<unsigned>& tab);
 // Runs the full inverse; returns (via *final) the buffer that holds +K^{-1}.
 // pivot0_done: pivot block 0 was already factored (by the assembly launch).
 hipError_t launch_spd_inverse(SpdArgs* args, int nmat, double** final_out, hipStream_t s,

@@ -55,7 +55,8 @@ constexpr int SS = 65;   // 64x64 LDS tile stride (doubles)
 
 struct BigSpdBatch {
   double* X[2];      // the matrix, inverted in place
-  double* Z[2];      // 2 x [W][p] panel, double-buffered by sweep parity (zbuf)
+  double* Z[2];      // 3 x [W][p] panel by sweep mod 3 (zbuf: a two-sweep tile update reads
+                     // panels k - 1 and k while the launch writes k + 1)
   double* Li[2];     // [W][W] L^{-1} of the current pivot block (row-major, zero upper) + scratch
   double* ldet[2];   // [p/32]
   double* pst[2];    // refinement gate [2]
@@ -66,6 +67,8 @@ struct BigSpdBatch {
   int G;                 // tile workgroups per factor in the update launch
   int nmat;
   int no_quarters;       // (SpdArgs::no_quarters)
+  const unsigned* sched[2];  // 128-wide update schedule (wide_schedule), stride sstride
+  int sstride;
 };
 
 __device__ __forceinline__ int bw(int p, int I) { return min(BW, p - BW * I); }
@@ -200,11 +203,11 @@ template <int R>
 constexpr int panel_lds() { return 32 * 65 + 2 * R * 32 * PB; }
 constexpr int PIVOT_LDS = pivot_lds<2>() > panel_lds<2>() ? pivot_lds<2>() : panel_lds<2>();  // doubles
 
-// the panel buffer of sweep k (the update of sweep k reads it while the panel of sweep k + 1 is
-// written into the other one, by the same launch)
+// the panel buffer of sweep k (the update of sweep k reads it -- and panel k - 1, for tiles that
+// apply two sweeps -- while the panel of sweep k + 1 is written into the third, by the same launch)
 template <int R>
 __device__ __forceinline__ double* zbuf(const BigSpdBatch& b, int m, int k) {
-  return b.Z[m] + (size_t)(k & 1) * (BW * R) * b.p[m];
+  return b.Z[m] + (size_t)(k % 3) * (BW * R) * b.p[m];
 }
 
 // inter-workgroup hand-off (MI355X_MICROARCH §inter-workgroup visibility, plain stores + agent
@@ -795,14 +798,16 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   const bool quarters = !b.no_quarters && full_rounds >= 1 && rem_tiles > 0 && 4 * rem_tiles <= nx;
   // item j of this workgroup -> (factor m, tile ti, tj, quarter qq: -1 = whole tile); false past
   // its run
-  auto tile_at = [&](int j, int& m, int& ti, int& tj, int& qq) -> bool {
+  auto tile_at = [&](int j, int& m, int& ti, int& tj, int& qq, unsigned& ent) -> bool {
     qq = -1;
+    ent = 0u;
     if (pivot) {
       if (j > 0) return false;
       m = L - first;
       const int T2 = (b.p[m] + WT - 1) / WT;
       if (k + 1 >= T2 || skip_pivot) return false;
       ti = tj = k + 1;
+      if (b.sched[m]) ent = b.sched[m][(size_t)k * b.sstride + 1];
       return true;
     }
     int loc;
@@ -824,6 +829,14 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     const int nt = T2 * (T2 + 1) / 2;
     const int Q = k + 1, qlin = Q * (Q + 1) / 2 + Q;
     int lin = wi % gx;
+    if (b.sched[m]) {  // the two-sweep schedule's list of this sweep
+      const unsigned* row = b.sched[m] + (size_t)k * b.sstride;
+      if (lin >= (int)row[0]) return false;
+      ent = row[2 + lin];
+      ti = (int)((ent >> 8) & 0xffu);
+      tj = (int)(ent & 0xffu);
+      return true;
+    }
     if (lin >= nt - (has_next ? 1 : 0)) return false;
     if (has_next && !skip_pivot) {  // the next panel row's tiles first (wide_tile_at)
       wide_tile_at(lin, T2, Q, true, ti, tj);
@@ -837,7 +850,8 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   double* sA0 = sm;
   double* sB0 = sm + 2 * SZ;
   int m, ti, tj, qq;
-  if (!tile_at(0, m, ti, tj, qq)) return;
+  unsigned ent;
+  if (!tile_at(0, m, ti, tj, qq, ent)) return;
   int j = 0;
   for (; qq < 0; ++j) {
     if (probe && !pivot && j < 2) {  // (trace build) round-0/1 phases over every tile workgroup
@@ -857,15 +871,25 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
     // the workgroup's next item
     int m2 = 0, ti2 = 0, tj2 = 0, q2 = -1;
-    const bool next = tile_at(j + 1, m2, ti2, tj2, q2);
+    unsigned ent2 = 0u;
+    const bool next = tile_at(j + 1, m2, ti2, tj2, q2, ent2);
     // The accumulators start at the tile's current values NEGATED (zero base in the swept blocks;
     // clamped addresses: rows / columns past p are never stored) and the product is added; the
     // store negates back: base - Z_I^T Z_J with the rounding of a subtraction (round-to-nearest
     // commutes with negation), and no separate base registers.  The base loads are issued ahead
     // of the product loop's first K-step.
+    // Two-sweep schedule (b.sched): new = c0 X + c1 Z_{k-1}^T Z_{k-1} + c2 Z_k^T Z_k, the
+    // coefficients (0, +-1) composing the sweeps' rules (wide_schedule); the products scale the
+    // A operand by c1 / c2 (exact).  One sweep (c1 = 0): the same operations as the form below,
+    // negated throughout -- bitwise the same values.  Without a schedule: the accumulators start
+    // at the tile NEGATED (zero base in the swept blocks) and the store negates back.
+    const bool sch = b.sched[m] != nullptr;
+    const bool two = sch && ((ent >> 16) & 1u);
+    auto cf = [](unsigned c) { return c == 0u ? 0.0 : c == 1u ? 1.0 : -1.0; };
+    const double c0 = cf((ent >> 18) & 3u), c1 = cf((ent >> 20) & 3u), c2 = cf((ent >> 22) & 3u);
     d4 acc[4][4];
     {
-      const double f = (inPi || inPj) ? -0.0 : -1.0;
+      const double f = sch ? c0 : ((inPi || inPj) ? -0.0 : -1.0);
 #pragma unroll
       for (int bx = 0; bx < 4; ++bx)
 #pragma unroll
@@ -879,7 +903,13 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     }
     // acc += Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j]) -- both
     // mn-contiguous, staged [k][mn] without a transpose (tile::product<1, 0>)
-    tile::product<1, 0, false, 0>(Z, p, Z, p, wK, p, p, i0, j0, 1.0, sm, t, wr, wc, lane, acc);
+    // (one call for every case -- a second inlined product loop spilled the accumulators: two
+    // sweeps read panel k - 1, always 128 deep since it is not the last sweep, then panel k)
+    {
+      const double* Zp = two ? zbuf<2>(b, m, k - 1) : Z;
+      tile::product2<1, 0>(Zp, Zp, two ? WT : 0, c1, Z, Z, wK, sch ? c2 : 1.0, p, p, p, p, i0, j0, sm, t,
+                           wr, wc, lane, acc);
+    }
     if (probe && !pivot && j < 2) TR_HI(SLOT_BIG_R0START + 3 * j + 2);
     double mx = 0.0;
 #pragma unroll
@@ -891,7 +921,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
           const int row = i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r;
           const int col = j0 + 64 * wc + 16 * by + (lane & 15);
           if (row < p && col < p) {
-            const double v = -sgn * acc[bx][by][r];
+            const double v = sch ? acc[bx][by][r] : -sgn * acc[bx][by][r];
             X[(size_t)row * p + col] = v;
             if (LAST && row == col && row < b.n[m]) mx = fmax(mx, v);
           }
@@ -923,6 +953,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     ti = ti2;
     tj = tj2;
     qq = q2;
+    ent = ent2;
   }
   // the quarter item (qq = 2 qi + qj): rows WT ti + 64 qi, columns WT tj + 64 qj; this wave's
   // 32 x 32 block (wr, wc) as 2 x 2 MFMA blocks, 16-deep K-steps through the same double-buffered
@@ -942,9 +973,15 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     const bool inPi = ti == k, inPj = tj == k;
     const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
     const int li = lane & 15, lk = lane >> 4;
+    // schedule (as the whole tiles): v = c0 X + c1 Z_{k-1}^T Z_{k-1} + c2 Z_k^T Z_k
+    const bool sch = b.sched[m] != nullptr;
+    const bool two = sch && ((ent >> 16) & 1u);
+    auto cf = [](unsigned c) { return c == 0u ? 0.0 : c == 1u ? 1.0 : -1.0; };
+    const double c0 = cf((ent >> 18) & 3u), c1 = cf((ent >> 20) & 3u), c2 = cf((ent >> 22) & 3u);
+    const double* Zp = two ? zbuf<2>(b, m, k - 1) : Z;
     d4 acc[2][2];
     {
-      const double f = (inPi || inPj) ? 0.0 : 1.0;
+      const double f = sch ? -c0 : ((inPi || inPj) ? 0.0 : 1.0);
 #pragma unroll
       for (int bx = 0; bx < 2; ++bx)
 #pragma unroll
@@ -960,30 +997,36 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     // c < 64: two 16-B loads per operand and thread, 512 B per k row (coalesced); the next
     // K-step's loads in flight under the current one's MFMAs.  (All K-steps' loads up front --
     // one round trip per item -- measured slower: 121 vs 113 us per update launch.)
-    auto qfetch = [&](double2 (&ra)[2], double2 (&rb)[2], int k0) {
+    // (two sweeps: K-steps [0, WT / KS) read panel k - 1 scaled by c1, the rest panel k by c2;
+    // the A operand is staged negated: acc = -(c0 X + ...), stored negated back by sgn below)
+    const int nk1 = two ? WT / KS : 0;
+    auto qfetch = [&](double2 (&ra)[2], double2 (&rb)[2], int kt) {
+      const double* Zs = kt < nk1 ? Zp : Z;
+      const int k0 = (kt < nk1 ? kt : kt - nk1) * KS;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int e = t + 256 * q, kr = e >> 5, c = 2 * (e & 31);
-        ra[q] = ld2(Z + (size_t)(k0 + kr) * p + min(i0 + c, p - 2));
-        rb[q] = ld2(Z + (size_t)(k0 + kr) * p + min(j0 + c, p - 2));
+        ra[q] = ld2(Zs + (size_t)(k0 + kr) * p + min(i0 + c, p - 2));
+        rb[q] = ld2(Zs + (size_t)(k0 + kr) * p + min(j0 + c, p - 2));
       }
     };
-    auto qstore = [&](const double2 (&ra)[2], const double2 (&rb)[2], double* sA, double* sB) {
+    auto qstore = [&](const double2 (&ra)[2], const double2 (&rb)[2], double* sA, double* sB, int kt) {
+      const double sa = sch ? (kt < nk1 ? -c1 : -c2) : -1.0;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int e = t + 256 * q, kr = e >> 5, c = 2 * (e & 31);
-        *reinterpret_cast<double2*>(sA + kr * S + c) = make_double2(-ra[q].x, -ra[q].y);
+        *reinterpret_cast<double2*>(sA + kr * S + c) = make_double2(sa * ra[q].x, sa * ra[q].y);
         *reinterpret_cast<double2*>(sB + kr * S + c) = rb[q];
       }
     };
-    const int nk = wK / KS;
+    const int nk = nk1 + wK / KS;
     double2 ra[2], rb[2];
     qfetch(ra, rb, 0);
-    qstore(ra, rb, sA0, sB0);
+    qstore(ra, rb, sA0, sB0, 0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
-      if (kt + 1 < nk) qfetch(ra, rb, (kt + 1) * KS);
+      if (kt + 1 < nk) qfetch(ra, rb, kt + 1);
       const double* sA = sA0 + cur * SZ;
       const double* sB = sB0 + cur * SZ;
 #pragma unroll
@@ -1003,7 +1046,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
           for (int y = 0; y < 2; ++y)
             acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], bb[y], acc[x][y], 0, 0, 0);
       }
-      if (kt + 1 < nk) qstore(ra, rb, sA0 + (cur ^ 1) * SZ, sB0 + (cur ^ 1) * SZ);
+      if (kt + 1 < nk) qstore(ra, rb, sA0 + (cur ^ 1) * SZ, sB0 + (cur ^ 1) * SZ, kt + 1);
       __syncthreads();
     }
     double mx = 0.0;
@@ -1016,7 +1059,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
           const int row = i0 + 32 * wr + 16 * bx + lk + 4 * r;
           const int col = j0 + 32 * wc + 16 * by + li;
           if (row < p && col < p) {
-            const double v = sgn * acc[bx][by][r];
+            const double v = sch ? -acc[bx][by][r] : sgn * acc[bx][by][r];
             X[(size_t)row * p + col] = v;
             if (LAST && row == col && row < b.n[m]) mx = fmax(mx, v);
           }
@@ -1054,6 +1097,78 @@ __global__ __launch_bounds__(256) void big_mirror_kernel(BigSpdBatch b) {
 
 int batch_R(const SpdArgs* a) { return a[0].wide ? 2 : 1; }
 
+}  // namespace
+
+// ---- the two-sweep schedule of the 128-wide update (round 5) -------------------------------
+// A sweep's update reads and writes every lower tile once for K = 128 of MFMA work; a tile that
+// takes two sweeps in one pass (K = 256) halves that traffic per flop.  Tiles are split into two
+// classes by the parity of I + J: class c applies sweeps in pairs (k - 1, k) in the launches with
+// k = c (mod 2), so every launch has half the bulk at K = 256 under which the serial part (next
+// pivot, next panel) still runs.  A tile the next panel or pivot reads (row / column k + 1) is
+// brought fully up to date in launch k whatever its class, and the last launch flushes every tile.
+// Every tile is touched at least every other launch, so it never lags by more than one sweep:
+// its pending sweeps are {k} or {k - 1, k}.  Per sweep s a tile changes as
+//   X <- lam (beta X + gam Z_s^T Z_s):  beta = 0 when I or J = s (its old value is the panel's
+//   input), gam = +1 when exactly one of I, J = s, else -1; lam = -1 on the last sweep;
+// two sweeps compose to c0 X + c1 Z_{k-1}^T Z_{k-1} + c2 Z_k^T Z_k.  The panels k - 1 and k are
+// both live (zbuf: three buffers).
+int wide_sched_stride(int T2) { return 2 + T2 * (T2 + 1) / 2; }
+
+void wide_schedule(int T2, bool paired, std::vector<unsigned>& tab) {
+  const int S = wide_sched_stride(T2);
+  tab.assign((size_t)T2 * S, 0u);
+  auto eager = [&](int I, int J, int k) {  // row / column k + 1, the pivot tile included
+    const int Q = k + 1;
+    return Q < T2 && ((I == Q && J <= Q) || (J == Q && I > Q));
+  };
+  auto updated = [&](int I, int J, int k) {
+    if (k < 0) return true;
+    return !paired || k == T2 - 1 || eager(I, J, k) || ((I + J) & 1) == (k & 1);
+  };
+  auto code = [](int c) { return c == 0 ? 0u : c > 0 ? 1u : 3u; };
+  for (int k = 0; k < T2; ++k) {
+    unsigned* row = tab.data() + (size_t)k * S;
+    const int Q = k + 1;
+    auto entry = [&](int I, int J) -> unsigned {
+      const bool two = !updated(I, J, k - 1);  // last touched in launch k - 2: sweeps k - 1, k
+      auto rule = [&](int s, int& beta, int& gam, int& lam) {
+        const bool pi = I == s, pj = J == s;
+        beta = (pi || pj) ? 0 : 1;
+        gam = (pi != pj) ? 1 : -1;
+        lam = s == T2 - 1 ? -1 : 1;
+      };
+      int b2, g2, l2;
+      rule(k, b2, g2, l2);
+      int c0 = l2 * b2, c1 = 0;
+      const int c2 = l2 * g2;
+      bool t2 = false;
+      if (two) {
+        int b1, g1, l1;
+        rule(k - 1, b1, g1, l1);
+        c0 = l2 * b2 * l1 * b1;
+        c1 = l2 * b2 * l1 * g1;
+        t2 = c1 != 0;  // (beta2 = 0: sweep k overwrites what sweep k - 1 left; it needs only Z_k)
+      }
+      return (unsigned)J | ((unsigned)I << 8) | ((t2 ? 1u : 0u) << 16) | (code(c0) << 18) |
+             (code(t2 ? c1 : 0) << 20) | (code(c2) << 22);
+    };
+    int n = 0;
+    if (Q < T2) {  // the next panel's tiles first: row Q left of the diagonal, column Q below it
+      for (int J = 0; J < Q; ++J) row[2 + n++] = entry(Q, J);
+      for (int I = Q + 1; I < T2; ++I) row[2 + n++] = entry(I, Q);
+      row[1] = entry(Q, Q);
+    }
+    for (int I = 0; I < T2; ++I)
+      for (int J = 0; J <= I; ++J) {
+        if (Q < T2 && (I == Q || J == Q)) continue;  // listed above / the pivot workgroup's
+        if (updated(I, J, k)) row[2 + n++] = entry(I, J);
+      }
+    row[0] = (unsigned)n;
+  }
+}
+
+namespace {
+
 BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   BigSpdBatch b{};
   Tmax = 0;
@@ -1063,7 +1178,10 @@ BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   b.G = g_big_wgs.load() > 0 ? g_big_wgs.load() : 255;
   b.nmat = nmat;
   b.no_quarters = a[0].no_quarters;
+  b.sstride = wide_sched_stride((a[0].p + 127) / 128);
   for (int m = 0; m < nmat; ++m) {
+    b.sched[m] = a[m].wide ? a[m].sched : nullptr;
+    if ((a[m].p + 127) / 128 != (a[0].p + 127) / 128) b.sched[m] = nullptr;  // (one stride per batch)
     b.X[m] = a[m].X; b.Z[m] = a[m].Z ? a[m].Z : a[m].Y; b.Li[m] = a[m].piv;
     b.ldet[m] = a[m].ldet; b.pst[m] = a[m].pst; b.status[m] = a[m].status; b.flag[m] = a[m].flag;
     b.p[m] = a[m].p; b.n[m] = a[m].n; b.T[m] = (a[m].p + BW - 1) / BW;
@@ -1103,7 +1221,18 @@ void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int sta
                        skip_pivot);
   } else {
     const int k = stage >> 1, nsw = (Tmax + 1) / 2;
-    const int gx = wide_tiles(Tmax) - 1, per_xcd = (nmat * gx + 7) / 8;
+    int gx = wide_tiles(Tmax) - 1;
+    if (b.sched[0]) {  // this sweep's list length (the same schedule the device table holds)
+      static thread_local std::vector<unsigned> tab;
+      static thread_local int tab_T2 = -1;
+      const int T2 = nsw;
+      if (tab_T2 != T2) {
+        wide_schedule(T2, true, tab);
+        tab_T2 = T2;
+      }
+      gx = std::max(1, (int)tab[(size_t)k * wide_sched_stride(T2)]);
+    }
+    const int per_xcd = (nmat * gx + 7) / 8;
     // persistent tile workgroups: two per CU on all but the 8 CUs whose first-pass workgroup is a
     // pivot slot (8 nx in all, nx per XCD slot), never more than the tiles
     const int first = std::max(8, wide_cus() - 8);

@@ -134,6 +134,9 @@ typedef struct gpk_problem {
  * never (NO_DD_CONTRACTION). */
 #define GPK_FLAG_DD_CONTRACTION 131072
 #define GPK_FLAG_NO_DD_CONTRACTION 262144
+/* 128-wide SPD inverse (factors >= 3072): every lower tile takes every sweep in its own pass
+ * (default: tiles take sweeps in pairs, K = 256 per pass, half the tiles per launch). */
+#define GPK_FLAG_ONE_SWEEP_UPDATE 524288
 
 typedef struct gpk_handle gpk_handle;
 
@@ -292,6 +295,14 @@ int gpk_dgemm(int32_t variant, int32_t M, int32_t N, int32_t K, double alpha, co
               double alpha2, const double* A2, int32_t lda2, int32_t ta2, const double* B2,
               int32_t ldb2, int32_t tb2, double beta, const double* C0, double* C, int32_t ldc,
               int32_t iters, double* avg_us);
+
+/* The 128-wide SPD inverse's two-sweep update schedule (host only, no device): for T2 128-tiles
+ * per dimension, T2 rows of wide_sched_stride(T2) = 2 + T2 (T2 + 1) / 2 words -- per sweep k the
+ * tile count, the next pivot tile's entry, then the entries J | I << 8 | two << 16 | c0 << 18 |
+ * c1 << 20 | c2 << 22 (coefficient codes 0, 1 = +1, 3 = -1; the tile's new value is
+ * c0 X + c1 Z_{k-1}^T Z_{k-1} + c2 Z_k^T Z_k).  paired = 0: the one-sweep form.  Writes at most
+ * cap words; returns GPK_EINVAL when cap is too small.  For tests and tools. */
+int gpk_wide_schedule(int32_t T2, int32_t paired, uint32_t* out, int64_t cap);
 
 /* ---- Row-sharded 2D step across GPUs (the reference has no multi-GPU path).
  * Every rank holds the problem, forms both Kronecker factors' K, D, K^{-1} itself, and computes
