@@ -509,6 +509,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
     pa.x = h->x1; pa.n = L.n1; pa.p = P; pa.kc = h->kc;
     pa.Kinv = h->Kinv[0]; pa.alpha = h->alpha; pa.beta = h->beta; pa.R = h->R;
     pa.halfc = 0.5 * h->prob.logdet; pa.deriv = 2; pa.part = h->pgpart; pa.cls = h->cls[0];
+    pa.part_lo = h->pg_dd ? h->pgpart_lo : nullptr;
     TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 1, &pa, 1, h->bpa, h->sc, h->s, &tail), "pgrad"));
     stamp("pgrad_tail");
@@ -1624,8 +1625,8 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   // The kernel-parameter contraction in double-double on the large 2D factors (C5): there the
   // sum over classes cancels ~1e8-fold and the fp64 rounding of the derivative fields sets its
   // accuracy; at C4 it would cost the latency-bound step ~1 us and buys nothing
-  h->pg_dd = use_cls && L.dim == 2 && !shard && !(p->flags & GPK_FLAG_NO_DD_CONTRACTION) &&
-             (std::max(P1, P2) >= SPD_WIDE_MIN || (p->flags & GPK_FLAG_DD_CONTRACTION));
+  h->pg_dd = use_cls && !shard && !(p->flags & GPK_FLAG_NO_DD_CONTRACTION) &&
+             ((L.dim == 2 && std::max(P1, P2) >= SPD_WIDE_MIN) || (p->flags & GPK_FLAG_DD_CONTRACTION));
   if (h->pg_dd) {
     A_(h->pgpart_lo, (size_t)L.naxes * h->bpa * 3 * QMAX);
     A_(h->tgpart_lo, (size_t)L.naxes * h->tngpa * 3 * QMAX);

@@ -646,10 +646,11 @@ static void launch_pg_c(const PGradBatch& b, int naxes, int bpa, int q, int deri
   const int ublocks = b.tail.fused ? (tail_nu(b.tail.adam.L) + 255) / 256 : 0;
   dim3 grid(std::max(bpa, std::min(ublocks, 4096)), naxes + (b.tail.fused ? 2 : 0));
   // double-double contraction: class path, 2D, with the fused tail carrying the low parts
-  const bool ddc = CLS && !mode1d && b.tail.fused && b.tail.gpart_lo && b.ax[0].part_lo &&
-                   (naxes < 2 || b.ax[1].part_lo);
+  const bool ddc = CLS && b.tail.fused && b.tail.gpart_lo && b.ax[0].part_lo && (naxes < 2 || b.ax[1].part_lo);
   if (ddc) {
-    if (deriv == 2)
+    if (mode1d)
+      hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, true, CLS, true>), grid, dim3(256), 0, s, b, q, sc);
+    else if (deriv == 2)
       hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 2, false, CLS, true>), grid, dim3(256), 0, s, b, q, sc);
     else
       hipLaunchKernelGGL((pgrad_kernel<MATERN, COS, 1, false, CLS, true>), grid, dim3(256), 0, s, b, q, sc);

@@ -128,7 +128,7 @@ typedef struct gpk_problem {
 /* 128-wide SPD inverse: keep the update's last round of tiles whole (default: quarter tiles when
  * that round would leave most workgroups idle). Bitwise the same results. */
 #define GPK_FLAG_NO_QUARTER_TILES 65536
-/* Kernel-parameter contraction (2D, distance classes): the derivative fields and every sum after
+/* Kernel-parameter contraction (distance classes): the derivative fields and every sum after
  * them in double-double (default only for factors of >= 3072 points, where the contraction's
  * cancellation amplifies the fields' fp64 rounding ~1e8-fold), at any size (DD_CONTRACTION) or
  * never (NO_DD_CONTRACTION). */

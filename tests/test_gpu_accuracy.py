@@ -159,7 +159,7 @@ def test_training_regime_c4_on_step_fields():
         assert e < tol[k], (k, e, tol[k])
 
 
-@pytest.mark.parametrize("cid", ["C3", "C4"])
+@pytest.mark.parametrize("cid", ["C1", "C2", "C3", "C4"])
 def test_dd_contraction_against_yardstick(cid):
     """The double-double kernel-parameter contraction (pgrad.hip fields_dd, forced here with
     GPK_FLAG_DD_CONTRACTION; default only at >= 3072-point factors, C5): the loss and every
