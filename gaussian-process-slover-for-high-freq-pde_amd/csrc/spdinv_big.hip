@@ -1121,9 +1121,14 @@ void wide_schedule(int T2, bool paired, std::vector<unsigned>& tab) {
     const int Q = k + 1;
     return Q < T2 && ((I == Q && J <= Q) || (J == Q && I > Q));
   };
+  // Diagonal tile (k + 2, k + 2) is the pivot workgroup's own tile in launch k + 1, the head of
+  // that launch's serial chain (tile -> 128-pivot -> panel).  Bringing it up to date in launch k
+  // (one more K = 128 tile in the bulk of odd launches) leaves it one sweep, K = 128, in launch
+  // k + 1 instead of the pair (K = 256: 50 vs 32 us in the C5 timeline, tools/big_timeline.py).
+  auto pre_pivot = [&](int I, int J, int k) { return I == J && I == k + 2 && I < T2; };
   auto updated = [&](int I, int J, int k) {
     if (k < 0) return true;
-    return !paired || k == T2 - 1 || eager(I, J, k) || ((I + J) & 1) == (k & 1);
+    return !paired || k == T2 - 1 || eager(I, J, k) || pre_pivot(I, J, k) || ((I + J) & 1) == (k & 1);
   };
   auto code = [](int c) { return c == 0 ? 0u : c > 0 ? 1u : 3u; };
   for (int k = 0; k < T2; ++k) {

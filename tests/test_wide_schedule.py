@@ -92,3 +92,15 @@ def test_schedule_halves_the_passes():
     pairs = sum(int(decode(two[k][2 + i])[2]) for k in range(T2) for i in range(int(two[k][0])))
     assert w2 < 0.56 * w1
     assert pairs > 0.8 * w2
+
+
+@pytest.mark.parametrize("T2", [3, 8, 32])
+def test_pivot_tile_one_sweep(T2):
+    """The pivot workgroup's tile (k + 1, k + 1), first on the launch's serial chain, carries one
+    sweep (K = 128) in every launch of the paired schedule: it was brought up to date one
+    launch earlier."""
+    tab = schedule(T2, True)
+    for k in range(T2 - 1):
+        I, J, two = decode(tab[k][1])[:3]
+        assert (I, J) == (k + 1, k + 1)
+        assert not two, k
