@@ -126,6 +126,7 @@ struct gpk_handle {
   // fused step tail (pgrad launch): group counters / partials, boundary gap
   unsigned int *tcount = nullptr, *ttop = nullptr;
   double *tgpart = nullptr, *bgap = nullptr;
+  int bgap_parts = 1;                 // PrepArgs::bgap_parts
   int ttg = 0, tngpa = 0;
   std::vector<GemmDesc> hdescs;  // per-stage GEMM descriptors (kernel arguments)
   Stage st[kGemmStages];
@@ -244,6 +245,7 @@ static PrepArgs make_prep(gpk_handle* h, int apply) {
   P.Up = h->Up; P.bvals = h->bvals; P.bidx = h->bidx; P.nb = h->prob.nb;
   P.dim = L.dim; P.n1 = L.n1; P.n2 = L.n2; P.p2 = L.p2;
   P.bgap = h->bgap;
+  P.bgap_parts = h->bgap_parts;
   return P;
 }
 
@@ -391,6 +393,7 @@ static TailArgs make_tail(gpk_handle* h, int apply, bool refine = true) {
   f.params = h->params; f.grad = h->grad; f.m = h->m; f.v = h->v;
   f.losses = h->losses; f.loss_slot = h->loss_slot; f.diag = h->diag;
   f.bgap = h->bgap;
+  f.bgap_parts = h->bgap_parts;
   if (!refine) {  // fast graph: check that no refinement was needed
     for (int a = 0; a < L.naxes; ++a) f.watch[a] = h->pst[a];
     f.viol = h->viol;
@@ -1631,7 +1634,9 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     A_(h->pgpart_lo, (size_t)L.naxes * h->bpa * 3 * QMAX);
     A_(h->tgpart_lo, (size_t)L.naxes * h->tngpa * 3 * QMAX);
   }
-  A_(h->bgap, 1);
+  // boundary-gap parts (PrepArgs::bgap): one per BGAP_CHUNK entries of a 2D boundary
+  h->bgap_parts = L.dim == 2 ? std::min(BGAP_PARTS_MAX, std::max(1, (2 * L.n1 + 2 * L.n2 + BGAP_CHUNK - 1) / BGAP_CHUNK)) : 1;
+  A_(h->bgap, BGAP_PARTS_MAX);
   A_(h->snap, (size_t)3 * L.nparams);
   A_(h->snap_count, 1);
   A_(h->viol, 1);

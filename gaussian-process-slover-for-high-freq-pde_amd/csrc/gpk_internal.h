@@ -124,6 +124,7 @@ namespace gpk {
 // Per-step constants from the flat params (kernel constants per axis, tau, v, the Adam step
 // counter and bias corrections).  Computed inside the assembly kernel: every workgroup derives
 // its axis constants itself and workgroup (0, 0) publishes them for the later kernels.
+constexpr int BGAP_CHUNK = 2048, BGAP_PARTS_MAX = 16;
 struct PrepArgs {
   const double* params;
   int off_kp[2];       // start of (freq, log-ls, log-w) per axis
@@ -138,7 +139,12 @@ struct PrepArgs {
   // model_GP_solver_1d.py:101-106), taken here because the fused tail updates U in place
   const double* Up; const double* bvals; const int* bidx;
   int nb, dim, n1, n2, p2;
-  double* bgap;        // out [1]
+  // out [bgap_parts]: partial sums over consecutive chunks of BGAP_CHUNK boundary entries,
+  // added in order by the step's tail.  A large 2D boundary (C5: 16384 entries) is spread over
+  // the first bgap_parts workgroups of the class-value launch -- one load round trip each
+  // instead of eight in one workgroup, which held that launch at 28 us
+  double* bgap;
+  int bgap_parts;      // 1 .. BGAP_PARTS_MAX
   int skip;            // 1: this launch does not publish them (another launch of the step does)
   // first step of a batch, folded in (stepk.h StepBegin; all null otherwise): snap_count <- count
   // before this step's increment, *viol0 = 0, *slot0 = 0 (thread 0 of publish_prep), and the

@@ -52,7 +52,8 @@ struct FinalizeArgs {
   double* params; double* grad; double* m; double* v;
   double* losses; int* loss_slot;
   double* diag;              // [8]: loss, logdet1, logdet2, quad, egap, bgap
-  const double* bgap;        // [1] ||u_b - b||^2 at the start of the step (assembly launch)
+  const double* bgap;        // [bgap_parts] ||u_b - b||^2 at the start of the step (assembly
+  int bgap_parts;            // launch, PrepArgs::bgap), added in order
   // fast graph (refinement stages left out): the refinement gate of each axis is checked here
   // and an open one raises *viol, after which the host rolls the batch back and reruns it
   // with the refinement stages (gpk_step).  watch[a] = nullptr: not checked.

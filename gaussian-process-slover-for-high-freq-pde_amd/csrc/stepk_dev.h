@@ -64,7 +64,14 @@ __device__ inline void finalize_body(const FinalizeArgs& f, int part = 0) {
   if (do_loss) {  // (uniform)
     const double q0 = f.red_quad[t < f.nquad ? t : 0], e0 = f.red_egap[t < f.negap ? t : 0];
     const double l0 = lp[lk < nl ? lk : 0];
-    bgap = *f.bgap;  // boundary gap of U at the start of the step (assembly launch)
+    // boundary gap of U at the start of the step (assembly launch): its parts, in order
+    double bg[BGAP_PARTS_MAX];
+#pragma unroll
+    for (int i = 0; i < BGAP_PARTS_MAX; ++i) bg[i] = i < f.bgap_parts ? f.bgap[i] : 0.0;
+    bgap = bg[0];
+#pragma unroll
+    for (int i = 1; i < BGAP_PARTS_MAX; ++i)
+      if (i < f.bgap_parts) bgap += bg[i];
     quad = t < f.nquad ? q0 : 0.0;
     egap = t < f.negap ? e0 : 0.0;
     for (int i = t + 256; i < f.nquad; i += 256) quad += f.red_quad[i];
