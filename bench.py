@@ -171,7 +171,8 @@ def large_factors(steps=3):
             "spd_inverse_gflops": 2 * n ** 3 / (inv_us * 1e-6) / 1e9,
             "spd_update_tflops": tfl / (tus * 1e-6) / 1e12,
             # K-assembly at size: gather_kernel writes K (+ its kept copy) and D of both 4096^2
-            # factors from the class values and reads each element's class id (bytes it moves)
+            # factors from the class values and reads each element's class-id variant byte (the
+            # bytes it moves: 839 MB at C5)
             "assembly": {"kernel": "gather_wide_kernel (K, Kc, D of both factors from class values, nontemporal stores)",
                          "us": gus, "bytes": gby, "hbm_gbs": gby / (gus * 1e-6) / 1e9,
                          "hbm_frac": gby / (gus * 1e-6) / 1e9 / PEAK_HBM_GBS,

@@ -2690,8 +2690,9 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
   } else if (nm == "gather") {
     // the K-assembly launch of the class path (the large-factor step's, gpk_api.cpp
     // enqueue_assemble_inverse): K (+ jitter), its kept copy Kc (when the handle keeps one) and D
-    // written, the int32 class id of every element read -- the bytes it really moves; the class
-    // values (U doubles per field) are L2-resident gathers and not counted
+    // written, the class id of every element read (its variant byte ClassArgs::vidx where the
+    // handle built them, p >= 1024; else the int32 id) -- the bytes it really moves; the class
+    // values and cbase entries are L2-resident gathers and not counted
     if (h->cls[0].ncls <= 0) return fail(GPK_EINVAL, "gather: this handle does not use distance classes");
     for (int a = 0; a < L.naxes; ++a) {
       aa[a].cls = h->cls[a];
@@ -2702,7 +2703,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     launch = [&]() { return launch_gather_only(aa, L.naxes, h->s); };
     for (int a = 0; a < L.naxes; ++a) {
       const double P = a == 0 ? L.p1 : L.p2;
-      bytes += P * P * (4.0 + 8.0 + (h->Kc[a] ? 8.0 : 0.0) + (deriv ? 8.0 : 0.0));
+      bytes += P * P * ((h->cls[a].vidx ? 1.0 : 4.0) + 8.0 + (h->Kc[a] ? 8.0 : 0.0) + (deriv ? 8.0 : 0.0));
     }
   } else if ((nm == "write_stream" || nm == "write_stream_after_copy") && L.dim == 2) {
     // a pure write stream of the gather's bytes (hipMemsetD32 of K, Kc, D of both factors),
@@ -2772,7 +2773,7 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     (void)hipEventDestroy(e1);
     for (int a = 0; a < L.naxes; ++a) {
       const double P = a == 0 ? L.p1 : L.p2;
-      bytes += P * P * (4.0 + 8.0 + (h->Kc[a] ? 8.0 : 0.0) + (deriv ? 8.0 : 0.0));
+      bytes += P * P * ((h->cls[a].vidx ? 1.0 : 4.0) + 8.0 + (h->Kc[a] ? 8.0 : 0.0) + (deriv ? 8.0 : 0.0));
     }
     *avg_us = tot / iters;
     *alg_flops = 0.0;
