@@ -183,8 +183,10 @@ __global__ __launch_bounds__(256) void class_eval_kernel(AssembleBatch b, int q)
   __shared__ double sw[QMAX], sa[QMAX], so[QMAX], sol[QMAX];
   if (t < q) axis_component(b.prep, axis, q, t, sw[t], sa[t], so[t], sol[t]);
   if (blockIdx.x == 0 && axis == 0) publish_prep(b.prep, q, false);
-  // the boundary gap's parts, one per workgroup of axis 0 (host: bgap_parts <= the grid's x)
-  if (axis == 0 && !b.prep.skip && b.prep.bgap && (int)blockIdx.x < b.prep.bgap_parts) bgap_part(b.prep, blockIdx.x);
+  // the boundary gap's parts, one per workgroup of axis 0 (strided: every part is written
+  // whatever the grid's width)
+  if (axis == 0 && !b.prep.skip && b.prep.bgap)
+    for (int w = blockIdx.x; w < b.prep.bgap_parts; w += gridDim.x) bgap_part(b.prep, w);
   __syncthreads();
   if (TR_FIRST) TR_LO(SLOT_CLASS_EVAL);
   if (TR_LAST) TR_LO(SLOT_CEVAL_START);
