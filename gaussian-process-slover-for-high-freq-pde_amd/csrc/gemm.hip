@@ -339,12 +339,9 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
     b0 = ((nk * wv) >> 2) << 5;
     b1 = ((nk * (wv + 1)) >> 2) << 5;
   };
-  // wave 0 runs the epilogue: prefetch its operands now so their latency hides under the MFMAs
-  EpiIn ein[4] = {};
-  if (wv == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ein[r] = epi_fetch(d, i0 + (lane >> 4) + 4 * r, j0 + (lane & 15));
-  }
+  // wave wv runs the epilogue of the tile's rows lane / 16 + 4 wv (one output per lane): its
+  // operands are prefetched now so their latency hides under the MFMAs
+  const EpiIn ein = epi_fetch(d, i0 + (lane >> 4) + 4 * wv, j0 + (lane & 15));
   if (!open) return;  // uniform
   int b0, b1, c0 = 0, c1 = 0;
   range(d.K, b0, b1);
@@ -369,32 +366,42 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
   }
   __syncthreads();
   if (TR_LAST) TR_HI(tslot + 3);
-  if (wv != 0) return;
+  // the epilogue on all four waves (one output per lane each; wave 0 used to run all four rows
+  // in turn): the K quarters summed in fixed order, then the stage's epilogue and stores
   double alpha = d.alpha, alpha2 = d.alpha2;
   if (d.vscale) alpha *= sc->v;
   if (d.vscale2) alpha2 *= sc->v;
   const double vv = d.Y ? sc->v : 0.0;
   double red = 0.0, red2 = 0.0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int q = lane * 4 + r;
+  {
+    const int q = lane * 4 + wv;
     const double s1 = (part[0][0][q] + part[0][1][q]) + (part[0][2][q] + part[0][3][q]);
-    const int row = i0 + (lane >> 4) + 4 * r, col = j0 + (lane & 15);
+    const int row = i0 + (lane >> 4) + 4 * wv, col = j0 + (lane & 15);
     double c = alpha * s1;
     if (DUAL && d.K2) c += alpha2 * ((part[1][0][q] + part[1][1][q]) + (part[1][2][q] + part[1][3][q]));
-    c = epi_apply(d, c, ein[r], red, red2);
+    c = epi_apply(d, c, ein, red, red2);
     d.C[(size_t)row * d.ldc + col] = c;
-    epi_side(d, row, col, c, ein[r], vv);
+    epi_side(d, row, col, c, ein, vv);
   }
-  if (d.red) {
+  if (d.red || d.red2) {  // (uniform) the tile's partials: waves' terms in row order, then lanes
+    double* sred = smem + 2 * 4 * 256;  // (past `part`, which other waves may still be reading)
+    sred[wv * 64 + lane] = red;
+    sred[256 + wv * 64 + lane] = red2;
+    __syncthreads();
+    if (wv == 0) {
+      red = ((sred[lane] + sred[64 + lane]) + sred[128 + lane]) + sred[192 + lane];
+      red2 = ((sred[256 + lane] + sred[320 + lane]) + sred[384 + lane]) + sred[448 + lane];
+      if (d.red) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) red += __shfl_xor(red, o, 64);
-    if (lane == 0) d.red[blockIdx.x] = red;
-  }
-  if (d.red2) {
+        for (int o = 32; o > 0; o >>= 1) red += __shfl_xor(red, o, 64);
+        if (lane == 0) d.red[blockIdx.x] = red;
+      }
+      if (d.red2) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) red2 += __shfl_xor(red2, o, 64);
-    if (lane == 0) d.red2[blockIdx.x] = red2;
+        for (int o = 32; o > 0; o >>= 1) red2 += __shfl_xor(red2, o, 64);
+        if (lane == 0) d.red2[blockIdx.x] = red2;
+      }
+    }
   }
   if (TR_FIRST) TR_HI(tslot);
 }
