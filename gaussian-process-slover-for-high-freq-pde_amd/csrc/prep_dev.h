@@ -32,7 +32,8 @@ __device__ inline void copy_snapshot(const PrepArgs& P, int wg, int nwg) {
 // Part w of the boundary gap ||u_b - b||^2 (u_b = hstack(U[0,:], U[-1,:], U[:,0], U[:,-1]) in
 // 2D, u[Xind] in 1D; PrepArgs::bgap): entries w BGAP_CHUNK + [0, BGAP_CHUNK), then every
 // bgap_parts chunks; 8 entries per thread per chunk, their loads issued before the sums; fixed
-// order (thread sums, wave butterflies, waves in order).  One part: the whole sum.
+// order (thread sums, wave butterflies, waves in order).  One part: the whole sum.  Every caller
+// runs 256-thread workgroups (BGAP_CHUNK = 8 x 256).
 __device__ inline void bgap_part(const PrepArgs& P, int w) {
   const int t = threadIdx.x;
   const int parts = P.bgap_parts > 0 ? P.bgap_parts : 1;
