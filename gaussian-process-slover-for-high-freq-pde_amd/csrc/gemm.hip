@@ -321,11 +321,16 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
   const GemmDesc& d = batch.d[blockIdx.y];
   const int tn = d.N >> 4;
   const int tiles = (d.M >> 4) * tn;
-  if ((int)blockIdx.x >= tiles) return;
+  // XCD-major dealing: blocks b, b + 8, ... share an XCD (and its L2) and take consecutive tiles,
+  // i.e. whole 16-row blocks of op(A), so each XCD's L2 holds 1/8 of op(A)'s rows instead of all
+  // of them (a bijection of [0, gridDim.x) when it is a multiple of 8; else the identity)
+  const int gx = (int)gridDim.x, x = (int)blockIdx.x;
+  const int tile = (gx & 7) ? x : (x & 7) * (gx >> 3) + (x >> 3);
+  if (tile >= tiles) return;
   // refinement gate: its (scalar) load is issued first and overlaps the epilogue prefetch; a
   // closed gate ends the workgroup before any operand load (launch + one round trip)
   const bool open = gate_open(d.gate);
-  const int i0 = (blockIdx.x / tn) * 16, j0 = (blockIdx.x % tn) * 16;
+  const int i0 = (tile / tn) * 16, j0 = (tile % tn) * 16;
   // per-wave operand staging (one 16 x FS block, A then B), reused for the cross-wave partials
   __shared__ double smem[4 * 16 * FS];
   double(*part)[4][256] = reinterpret_cast<double(*)[4][256]>(smem);
@@ -394,12 +399,12 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
       if (d.red) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) red += __shfl_xor(red, o, 64);
-        if (lane == 0) d.red[blockIdx.x] = red;
+        if (lane == 0) d.red[tile] = red;
       }
       if (d.red2) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) red2 += __shfl_xor(red2, o, 64);
-        if (lane == 0) d.red2[blockIdx.x] = red2;
+        if (lane == 0) d.red2[tile] = red2;
       }
     }
   }
