@@ -38,6 +38,13 @@ enum TraceSlot {
   SLOT_MC_PUB = 192,    // the pass-0 tiles published (flags raised)
   SLOT_MC_DONE = 208,   // pass 1 done (end of the sweep)
   SLOT_MC_PROD = 224,   // pass-0 products done (before their stores)
+  // chain_multi_kernel, factor 0, sweep k < 16, every workgroup publishing panel row k + 1:
+  // [first, last] inputs (panel + L_k^{-1}) in, [first, last] pass 0 published.  These reuse the
+  // GEMM-stage and 128-wide-update slots, which a 1D (chain_multi) step never fires
+  SLOT_MCP_IN = 64, SLOT_MCP_OUT = 240,
+  // ... the last inputs-in and the last publication as (clock << 16 | blockIdx.x); the pivot
+  // chain's workgroup id (mpos)
+  SLOT_MCP_WHO_IN = 80, SLOT_MCP_WHO_OUT = 96, SLOT_MCP_MPOS = 112,
   // wide_update_kernel (spdinv_big.hip), sweep BIG_PROBE_SWEEP, factor 0: launch start (first
   // workgroup), pivot workgroup [start, its tile done], pivot128 done, panel workgroups [first
   // start, L^{-1} seen], panel done (last), tile workgroups' round 0 / 1 ends (max), quarter
@@ -73,6 +80,8 @@ constexpr int BIG_PROBE_SWEEP = 8;
    blockIdx.z == gridDim.z - 1)
 #define TR_LO(slot) atomicMin(&trace_lo[slot], (unsigned long long)wall_clock64())
 #define TR_HI(slot) atomicMax(&trace_hi[slot], (unsigned long long)wall_clock64())
+// the LAST arriving workgroup's id: (clock << 16 | id) under atomicMax (decoded by tools/timeline.py)
+#define TR_WHO(slot, id) atomicMax(&trace_hi[slot], ((unsigned long long)wall_clock64() << 16) | (unsigned)(id))
 #else
 #define GPK_TRACE_TU(tu)                                   \
   void trace_fetch_##tu(uint64_t* lo, uint64_t* hi) {      \
@@ -83,6 +92,7 @@ constexpr int BIG_PROBE_SWEEP = 8;
 #define TR_LAST false
 #define TR_LO(slot) ((void)0)
 #define TR_HI(slot) ((void)0)
+#define TR_WHO(slot, id) ((void)0)
 #endif
 
 void trace_fetch_assemble(uint64_t* lo, uint64_t* hi);

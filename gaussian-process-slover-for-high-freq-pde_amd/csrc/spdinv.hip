@@ -742,6 +742,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
   // pass over the CUs does not double up), the tile workgroups around it
   const int mpos = b.mpos < nwg ? b.mpos : 0;
   const bool master = (int)blockIdx.x == mpos;
+  if (master && threadIdx.x == 0 && m == 0) TR_WHO(SLOT_MCP_MPOS, blockIdx.x);
   int R = 0, c0 = -1, dmask = 0;
   if (!master) multi_role((int)blockIdx.x - ((int)blockIdx.x > mpos ? 1 : 0), R, c0, dmask);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -997,6 +998,15 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
       load_l();
     }
     if (trc) TR_HI(SLOT_MC_PIV + k);
+    // probes (trace build): every workgroup that publishes panel row k + 1 in this sweep's pass 0,
+    // [first, last] of its inputs-in and of its publication (SLOT_MCP_IN / SLOT_MCP_OUT)
+    [[maybe_unused]] bool pubk = false;
+#ifdef GPK_TRACE
+#pragma unroll
+    for (int s = 0; s < 7; ++s) pubk = pubk || (valid(s) && publishes(s, k + 1));
+    pubk = pubk && t == 0 && m == 0 && k < 16;
+    if (pubk) { TR_LO(SLOT_MCP_IN + k); TR_HI(SLOT_MCP_IN + k); TR_WHO(SLOT_MCP_WHO_IN + k, blockIdx.x); }
+#endif
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1060,6 +1070,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
       if (pass == 0 && trc) TR_HI(SLOT_MC_PROD + k);
       if (pass == 0 && k + 1 < T) publish_stores(k + 1);
       if (pass == 0 && trc) TR_HI(SLOT_MC_PUB + k);
+      if (pass == 0 && pubk) { TR_LO(SLOT_MCP_OUT + k); TR_HI(SLOT_MCP_OUT + k); TR_WHO(SLOT_MCP_WHO_OUT + k, blockIdx.x); }
       if (pass == 0) __builtin_amdgcn_s_setprio(0);
     }
     {  // reset chunk k of this workgroup's share of the other half

@@ -48,6 +48,13 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C4")
 ap.add_argument("--steps", type=int, default=5)
 a = ap.parse_args()
+if a.config in ("C1", "C2"):  # 1D: gpk_trace.h SLOT_MCP_IN / SLOT_MCP_OUT reuse the GEMM / update slots
+    for k in range(16):
+        for j in range(4):
+            NAMES.pop(64 + 4 * k + j, None)
+    for k in range(16):
+        NAMES[64 + k] = f"row {k + 1} publishers (sweep {k}): inputs in (first..last)"
+        NAMES[240 + k] = f"row {k + 1} publishers (sweep {k}): published (first..last)"
 if "GPK_LIB_PATH" not in os.environ:
     os.environ["GPK_LIB_PATH"] = os.path.join(ROOT, "gaussian-process-slover-for-high-freq-pde_amd",
                                               "gpk", "_lib", "libgpk_trace.so")
@@ -57,12 +64,35 @@ lib = _lib.load()
 s = problems.make_solver(a.config, seed=0)
 s.step(20)
 U64 = ctypes.c_uint64 * NS
+who = []
+
+
+def who_role(wg, mpos):
+    """chain_multi_kernel workgroup -> (macro row R, column pair c0, diagonal tiles) (spdinv.hip multi_role)"""
+    g = wg - (1 if wg > mpos else 0)
+    if g == 0:
+        return (0, -1, "d3")
+    r, first = 1, 1
+    while first + r <= g:
+        first += r
+        r += 1
+    c0 = g - first
+    o4, o5, o6 = (r - 2 if r >= 2 else 0), (r - 3 if r >= 3 else 0), r - 1
+    dm = "".join(n for n, o in (("(2R,2R)", o4), ("(2R+1,2R)", o5), ("(2R+1,2R+1)", o6)) if c0 == o)
+    return (r, c0, dm)
 acc_lo, acc_hi, cnt = np.zeros(NS), np.zeros(NS), np.zeros(NS)
 for _ in range(a.steps):
     _lib.check(lib.gpk_trace_reset())
     s.step(1)
     lo, hi = U64(), U64()
     _lib.check(lib.gpk_trace_read(lo, hi, NS))
+    if a.config in ("C1", "C2"):  # last publishers (clock << 16 | blockIdx.x), decoded as ids
+        raw = [int(v) for v in hi[:]]
+        mpos = raw[112] & 0xFFFF
+        who.append([(who_role(raw[80 + k] & 0xFFFF, mpos) if raw[80 + k] else None,
+                     who_role(raw[96 + k] & 0xFFFF, mpos) if raw[96 + k] else None) for k in range(16)])
+        for i in list(range(80, 113)):
+            hi[i] = 0
     lo = np.array(lo[:], dtype=np.float64)
     hi = np.array(hi[:], dtype=np.float64)
     valid_lo = lo < 2 ** 63
@@ -77,3 +107,8 @@ for i in sorted(range(NS), key=lambda i: (acc_lo[i] / max(cnt[i], 1)) if cnt[i] 
     if cnt[i]:
         l, h = acc_lo[i] / cnt[i], acc_hi[i] / cnt[i]
         print(f"  {str(NAMES.get(i, i)):24s} {l:9.2f} .. {h:9.2f}   ({h - l:7.2f})")
+if who:
+    print("last publisher of each panel row (macro row R, column pair c0, diagonal tiles held), per step:")
+    for k in range(16):
+        print(f"  row {k + 1:2d} (sweep {k:2d}): last in " + "; ".join(str(w[k][0]) for w in who)
+              + " | last out " + "; ".join(str(w[k][1]) for w in who))
