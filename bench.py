@@ -155,7 +155,9 @@ def large_factors(steps=3):
         us, fl, _ = s.bench_kernel("gemm_B", 5)
         inv_us = s.time_spd_inverse(3)
         n = 4096
-        tus, tfl, _ = s.bench_kernel("spd_tiles", 3)
+        # every update launch of one inverse (even and odd launches of the two-sweep schedule),
+        # credited the MFMA work their tile lists schedule (gpk_bench_kernel "spd_updates")
+        tus, tfl, _ = s.bench_kernel("spd_updates", 3)
         gus, _, gby = s.bench_kernel("gather", 5)
         # the same launch inside whole steps (stage 'assemble' = class_eval + the gather, HIP
         # events around the stage): the first gather after a step's GEMMs runs ~2x slower than
@@ -170,6 +172,9 @@ def large_factors(steps=3):
             "gemm_mfma_frac": gemm_tf / PEAK_F64_TFLOPS, "spd_inverse_ms": inv_us / 1e3,
             "spd_inverse_gflops": 2 * n ** 3 / (inv_us * 1e-6) / 1e9,
             "spd_update_tflops": tfl / (tus * 1e-6) / 1e12,
+            "spd_update_us": tus,
+            "spd_update_flops": "per update launch, averaged over one inverse's launches: the tile "
+                                "products its lists schedule (2 w_I w_J K, K = 128 or 256) + next pivot + panel",
             # K-assembly at size: gather_kernel writes K (+ its kept copy) and D of both 4096^2
             # factors from the class values and reads each element's class-id variant byte (the
             # bytes it moves: 839 MB at C5)

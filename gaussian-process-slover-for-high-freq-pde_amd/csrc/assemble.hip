@@ -390,9 +390,11 @@ __global__ __launch_bounds__(256) void gather_wide_kernel(AssembleBatch b, int n
   }
 }
 
-static void launch_gather_wide(const AssembleBatch& b, int naxes, int deriv, hipStream_t s) {
+static hipError_t launch_gather_wide(const AssembleBatch& b, int naxes, int deriv, hipStream_t s) {
+  // every axis needs its variant bytes (gpk_create builds them for all axes once max P >= 1024);
+  // an axis without them would be left unassembled, so refuse the launch
   for (int k = 0; k < naxes; ++k)
-    if (!b.ax[k].cls.vidx) return;  // (the handle builds them for p >= 1024; the launch fails below)
+    if (!b.ax[k].cls.vidx) return hipErrorInvalidValue;
   int pmax = 0;
   for (int k = 0; k < naxes; ++k) pmax = std::max(pmax, b.ax[k].p);
   const int nbx = (pmax + GW_COLS - 1) / GW_COLS, nby = (pmax + GW_ROWS - 1) / GW_ROWS, nblk = nbx * nby * naxes;
@@ -400,10 +402,11 @@ static void launch_gather_wide(const AssembleBatch& b, int naxes, int deriv, hip
   if (deriv == 2) hipLaunchKernelGGL((gather_wide_kernel<2>), g, dim3(256), 0, s, b, nbx, nby, nblk);
   else if (deriv == 1) hipLaunchKernelGGL((gather_wide_kernel<1>), g, dim3(256), 0, s, b, nbx, nby, nblk);
   else hipLaunchKernelGGL((gather_wide_kernel<0>), g, dim3(256), 0, s, b, nbx, nby, nblk);
+  return hipSuccess;
 }
 
 template <bool MATERN, bool COS>
-static void launch_class_t(const AssembleBatch& b, int naxes, int maxc, int maxtiles, int q,
+static hipError_t launch_class_t(const AssembleBatch& b, int naxes, int maxc, int maxtiles, int q,
                            int deriv, hipStream_t s, bool eval_only) {
   dim3 ge((maxc + 7) / 8, naxes), gg(naxes, maxtiles + (b.pivot_x >= 0 ? 1 : 0));
   // (no pivot-0 workgroup and large tiles: the streaming layout)
@@ -418,7 +421,8 @@ static void launch_class_t(const AssembleBatch& b, int naxes, int maxc, int maxt
     hipLaunchKernelGGL((class_eval_kernel<MATERN, COS, 0>), ge, dim3(256), 0, s, b, q);
     if (!eval_only && !wide) hipLaunchKernelGGL((gather_kernel<0>), gg, dim3(256), 0, s, b);
   }
-  if (!eval_only && wide) launch_gather_wide(b, naxes, deriv, s);
+  if (!eval_only && wide) return launch_gather_wide(b, naxes, deriv, s);
+  return hipSuccess;
 }
 
 // the gather launch alone (gpk_bench_kernel "gather": the K-assembly kernel's HBM rate); the
@@ -433,8 +437,8 @@ hipError_t launch_gather_only(const AssembleArgs* a, int naxes, hipStream_t s) {
   }
   b.pivot_x = -1;
   if (maxtiles >= GW_WIDE_MIN_TILES) {  // (what launch_assemble runs at this size)
-    launch_gather_wide(b, naxes, a[0].deriv, s);
-    return hipGetLastError();
+    const hipError_t e = launch_gather_wide(b, naxes, a[0].deriv, s);
+    return e != hipSuccess ? e : hipGetLastError();
   }
   dim3 gg(naxes, maxtiles);
   if (a[0].deriv == 2) hipLaunchKernelGGL((gather_kernel<2>), gg, dim3(256), 0, s, b);
@@ -548,13 +552,14 @@ hipError_t launch_assemble(int kind, int q, const AssembleArgs* a, int naxes, co
       maxc = std::max(maxc, a[k].cls.ncls);
     }
     b.pivot_x = a[0].piv ? maxtiles : -1;
+    hipError_t e;
     switch (kind) {
-      case SE_COS: launch_class_t<false, true>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
-      case MATERN52_COS: launch_class_t<true, true>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
-      case SE: launch_class_t<false, false>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
-      default: launch_class_t<true, false>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
+      case SE_COS: e = launch_class_t<false, true>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
+      case MATERN52_COS: e = launch_class_t<true, true>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
+      case SE: e = launch_class_t<false, false>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
+      default: e = launch_class_t<true, false>(b, naxes, maxc, maxtiles, q, deriv, s, eval_only); break;
     }
-    return hipGetLastError();
+    return e != hipSuccess ? e : hipGetLastError();
   }
   b.pivot_x = a[0].piv ? maxt * ASM_SUB : -1;
   switch (kind) {

@@ -1597,7 +1597,10 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
         return bail(fail(GPK_EHIP, "upload distance classes"));
       c.ncls = U; c.vmax = vmax[a]; c.dist = dist; c.cid = cid; c.cbase = cb;
       c.kval = kval; c.dval = dval; c.nchunk = nchunk; c.rb = rb; c.part = part;
-      if (P >= 1024) {  // the large-factor gather's variant bytes (ClassArgs::vidx)
+      // the large-factor gather's variant bytes (ClassArgs::vidx), for EVERY axis once the
+      // largest one takes gather_wide_kernel (assemble.hip: (P/32)^2 >= GW_WIDE_MIN_TILES, i.e.
+      // max P >= 1024) -- that launch assembles all axes at once
+      if (std::max(P1, L.naxes == 2 ? P2 : 0) >= 1024) {
         std::vector<unsigned char> vb((size_t)P * P, 0xff);
         for (int i = 0; i < n; ++i)
           for (int j = 0; j < n; ++j) {
@@ -2024,6 +2027,28 @@ int gpk_sync(gpk_handle* h) {
   return GPK_OK;
 }
 
+// gpk_set_wait_limit_chunk: the poll budget applied while gpk_step runs one chunk of a call
+// (tests: a failure in a later chunk leaves the earlier chunks applied)
+static std::atomic<int> g_chunk_limit_polls{0}, g_chunk_limit_at{-1};
+struct ChunkWaitLimit {
+  bool on = false;
+  ChunkWaitLimit(gpk_handle* h, int chunk) {
+    if (g_chunk_limit_polls.load() <= 0 || chunk != g_chunk_limit_at.load()) return;
+    // (the previous chunk's tail may still run: the limit must not reach its waits)
+    on = hipStreamSynchronize(h->s) == hipSuccess && gpk_set_wait_limit(g_chunk_limit_polls.load()) == GPK_OK;
+  }
+  ~ChunkWaitLimit() {
+    if (on) gpk_set_wait_limit(0);
+  }
+};
+
+int gpk_set_wait_limit_chunk(int32_t polls, int32_t chunk) {
+  if (polls < 0) return fail(GPK_EINVAL, "polls must be >= 0");
+  g_chunk_limit_polls.store(polls);
+  g_chunk_limit_at.store(polls > 0 ? chunk : -1);
+  return GPK_OK;
+}
+
 int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
   if (!h) return fail(GPK_EINVAL, "NULL handle");
   if (n_steps < 0) return fail(GPK_EINVAL, "n_steps < 0");
@@ -2050,7 +2075,8 @@ int gpk_step(gpk_handle* h, int32_t n_steps, double* losses) {
     if (losses) std::memcpy(losses, h->rep_host + 8, sizeof(double));
     return read_report(h, false, &viol);
   }
-  while (done < n_steps) {
+  for (int chunk = 0; done < n_steps; ++chunk) {
+    ChunkWaitLimit chunk_limit(h, chunk);  // (tests: gpk_set_wait_limit_chunk)
     // (both graphs run in FAST_CHUNK chunks while the fast graph is available, so the mode is
     // re-decided every 64 steps: a long first call on the full graph used to keep its whole
     // length there, and the training that followed, until the gate bound fell below the entry
@@ -2103,8 +2129,10 @@ int gpk_prepare(gpk_handle* h, int32_t n_steps) {
     TRY(capture(h, 1, refine != 0));
     if (!h->shard) TRY(capture_call(h, refine == 0));
     if (!h->shard && n_steps >= STEP_GRAPH_REPS) TRY(capture(h, 1, refine != 0, STEP_GRAPH_REPS));
-    // the chunks of a call of n_steps (fast: FAST_CHUNK-step chunks + the remainder; the full
-    // graph runs them as one batch, decomposed the same way), one graph each
+    // the chunks of a call of n_steps: FAST_CHUNK-step chunks + the remainder whenever the fast
+    // graph exists (fast_ok), on either graph -- each chunk is a batch of its own (snapshot,
+    // report, undo on failure); without a fast graph the whole call is one batch, run as
+    // kBatchMax-step graphs + the remainder.  One graph each
     if (!h->shard && n_steps > STEP_GRAPH_REPS) {
       const int full = std::min(n_steps, kBatchMax), rest = n_steps % kBatchMax;
       TRY(capture(h, 1, refine != 0, full, true));
@@ -2647,10 +2675,12 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    // n^3 per factor over its ceil(p/64) sweeps; HBM: read + write the lower triangle
+    // the MFMA work launch 0 schedules (its tile lists: under the two-sweep schedule launch 0
+    // updates only its own parity class + the eager row / column, all at K = 128), + the next
+    // pivot and panel; HBM: read + write the lower triangle
+    flops = spd_big_update_flops(sa, L.naxes, 0, true);
     for (int a = 0; a < L.naxes; ++a) {
       const double n = a == 0 ? n1 : n2;
-      flops += n * n * n / spd_big_sweeps(a == 0 ? L.p1 : L.p2, h->bigwide);
       bytes += 8.0 * n * n;
     }
     *avg_us = tot / iters;
@@ -2664,11 +2694,47 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
     TRY(check_launch(launch_spd_big_stage(sa, L.naxes, -1, h->s), "pivot_init"));
     TRY(check_launch(launch_spd_big_stage(sa, L.naxes, 0, h->s), "panel"));
     launch = [&]() { return launch_spd_big_tiles(sa, L.naxes, 0, h->s); };
+    // the tile products launch 0's lists schedule (no pivot workgroup) -- the work actually done
+    flops = spd_big_update_flops(sa, L.naxes, 0, false);
     for (int a = 0; a < L.naxes; ++a) {
       const double n = a == 0 ? n1 : n2;
-      flops += n * n * n / spd_big_sweeps(a == 0 ? L.p1 : L.p2, h->bigwide);
       bytes += 8.0 * n * n;
     }
+  } else if (nm == "spd_updates" && h->bigspd) {
+    // every update launch of one inverse (sweeps 0 .. last, each with its fused next pivot and
+    // panel; the final mirror left out), between two events after pivot 0 and panel 0: the
+    // average update launch as the step runs it, even and odd launches of the two-sweep schedule
+    // alike, credited with the work their tile lists schedule (spd_big_update_flops)
+    int nsw = 0;
+    for (int a = 0; a < L.naxes; ++a) nsw = std::max(nsw, spd_big_sweeps(a == 0 ? L.p1 : L.p2, h->bigwide));
+    for (int k = 0; k < nsw; ++k) flops += spd_big_update_flops(sa, L.naxes, k, true);
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    double tot = 0.0;
+    for (int it = 0; it < iters; ++it) {
+      TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
+      TRY(check_launch(launch_spd_big_stage(sa, L.naxes, -1, h->s), "pivot_init"));
+      TRY(check_launch(launch_spd_big_stage(sa, L.naxes, 0, h->s), "panel"));
+      HIPCHK(hipEventRecord(e0, h->s));
+      for (int k = 0; k < nsw; ++k)
+        TRY(check_launch(launch_spd_big_stage(sa, L.naxes, 2 * k + 1, h->s, false), "update"));
+      HIPCHK(hipEventRecord(e1, h->s));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      tot += ms * 1000.0;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (int a = 0; a < L.naxes; ++a) {  // read + write the lower triangle per sweep
+      const double n = a == 0 ? n1 : n2;
+      bytes += 8.0 * n * n * spd_big_sweeps(a == 0 ? L.p1 : L.p2, h->bigwide);
+    }
+    *avg_us = tot / iters / nsw;  // per update launch
+    *alg_flops = flops / nsw;
+    *alg_bytes = bytes / nsw;
+    return read_status(h);
   } else if ((nm == "spd_pivot" || nm == "spd_panel") && h->bigspd) {
     // large path pieces (idempotent): the 64-pivot factorisation of block 0, the panel of sweep 0
     TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, make_prep(h, 0), h->s), "assemble"));
@@ -2899,14 +2965,17 @@ int gpk_dgemm(int32_t variant, int32_t M, int32_t N, int32_t K, double alpha, co
     if (e == hipSuccess) {
       e = hipEventCreate(&e1);
       if (e == hipSuccess) {
-        (void)launch();  // warm
-        (void)hipEventRecord(e0, 0);
+        // (timing only: with C0 == C every timed launch updates dC in place, so each one reads
+        // the previous launch's output as its C0 -- same shapes and work, different values; the
+        // result copied back above is the first launch's)
+        e = launch();  // warm
+        if (e == hipSuccess) e = hipEventRecord(e0, 0);
         for (int it = 0; it < iters && e == hipSuccess; ++it) e = launch();
-        (void)hipEventRecord(e1, 0);
+        if (e == hipSuccess) e = hipEventRecord(e1, 0);
         if (e == hipSuccess) e = hipEventSynchronize(e1);
         float ms = 0.f;
         if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-        *avg_us = ms * 1000.0 / iters;
+        if (e == hipSuccess) *avg_us = ms * 1000.0 / iters;  // (untouched on failure)
         (void)hipEventDestroy(e1);
       }
       (void)hipEventDestroy(e0);

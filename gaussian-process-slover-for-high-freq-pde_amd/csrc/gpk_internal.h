@@ -333,7 +333,10 @@ hipError_t wait_limit_spdbig(unsigned polls);
 hipError_t wait_limit_assemble(unsigned polls);
 hipError_t launch_spd_inverse_big(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
 // stage -1: pivot 0; 2k: panel of sweep k; 2k+1: update of sweep k
-hipError_t launch_spd_big_stage(SpdArgs* args, int nmat, int stage, hipStream_t s);
+// (mirror = false: the last update launch leaves the upper triangle unmirrored -- bench timing)
+hipError_t launch_spd_big_stage(SpdArgs* args, int nmat, int stage, hipStream_t s, bool mirror = true);
+// MFMA work of update launch k as scheduled (bench accounting; spdinv_big.hip)
+double spd_big_update_flops(const SpdArgs* args, int nmat, int k, bool with_pivot);
 hipError_t launch_spd_big_tiles(SpdArgs* args, int nmat, int k, hipStream_t s);  // bench only
 int spd_big_sweeps(int p, int wide);
 

@@ -67,8 +67,8 @@ struct BigSpdBatch {
   int G;                 // tile workgroups per factor in the update launch
   int nmat;
   int no_quarters;       // (SpdArgs::no_quarters)
-  const unsigned* sched[2];  // 128-wide update schedule (wide_schedule), stride sstride
-  int sstride;
+  const unsigned* sched[2];  // 128-wide update schedule (wide_schedule) per factor, row stride sstride[m]
+  int sstride[2];
 };
 
 __device__ __forceinline__ int bw(int p, int I) { return min(BW, p - BW * I); }
@@ -807,7 +807,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
       const int T2 = (b.p[m] + WT - 1) / WT;
       if (k + 1 >= T2 || skip_pivot) return false;
       ti = tj = k + 1;
-      if (b.sched[m]) ent = b.sched[m][(size_t)k * b.sstride + 1];
+      if (b.sched[m]) ent = b.sched[m][(size_t)k * b.sstride[m] + 1];
       return true;
     }
     int loc;
@@ -830,7 +830,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     const int Q = k + 1, qlin = Q * (Q + 1) / 2 + Q;
     int lin = wi % gx;
     if (b.sched[m]) {  // the two-sweep schedule's list of this sweep
-      const unsigned* row = b.sched[m] + (size_t)k * b.sstride;
+      const unsigned* row = b.sched[m] + (size_t)k * b.sstride[m];
       if (lin >= (int)row[0]) return false;
       ent = row[2 + lin];
       ti = (int)((ent >> 8) & 0xffu);
@@ -1174,6 +1174,15 @@ void wide_schedule(int T2, bool paired, std::vector<unsigned>& tab) {
 
 namespace {
 
+// the host copy of wide_schedule(T2, paired) -- the table gpk_create uploads per factor -- cached
+// per T2 (per host thread: handles of an in-process group launch from several threads)
+const std::vector<unsigned>& host_wide_schedule(int T2) {
+  static thread_local std::vector<std::vector<unsigned>> cache;
+  if ((int)cache.size() <= T2) cache.resize(T2 + 1);
+  if (cache[T2].empty()) wide_schedule(T2, true, cache[T2]);
+  return cache[T2];
+}
+
 BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   BigSpdBatch b{};
   Tmax = 0;
@@ -1183,10 +1192,11 @@ BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   b.G = g_big_wgs.load() > 0 ? g_big_wgs.load() : 255;
   b.nmat = nmat;
   b.no_quarters = a[0].no_quarters;
-  b.sstride = wide_sched_stride((a[0].p + 127) / 128);
   for (int m = 0; m < nmat; ++m) {
+    // every factor keeps its own schedule (built for its own T2 = ceil(p / 128)); the update
+    // launch's per-factor item count covers the longest list (launch_stage_r)
     b.sched[m] = a[m].wide ? a[m].sched : nullptr;
-    if ((a[m].p + 127) / 128 != (a[0].p + 127) / 128) b.sched[m] = nullptr;  // (one stride per batch)
+    b.sstride[m] = wide_sched_stride((a[m].p + 127) / 128);
     b.X[m] = a[m].X; b.Z[m] = a[m].Z ? a[m].Z : a[m].Y; b.Li[m] = a[m].piv;
     b.ldet[m] = a[m].ldet; b.pst[m] = a[m].pst; b.status[m] = a[m].status; b.flag[m] = a[m].flag;
     b.p[m] = a[m].p; b.n[m] = a[m].n; b.T[m] = (a[m].p + BW - 1) / BW;
@@ -1208,15 +1218,9 @@ int wide_cus() {
   return cached;
 }
 
-// workgroups of one 128-wide update launch: the pivot workgroup + one per lower 128-tile
-int wide_tiles(int Tmax) {
-  const int T2 = (Tmax + 1) / 2;
-  return 1 + T2 * (T2 + 1) / 2;
-}
-
 template <int R>
 void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int stage, hipStream_t s,
-                    int skip_pivot = 0) {
+                    int skip_pivot = 0, bool mirror = true) {
   if (stage < 0) {
     hipLaunchKernelGGL(big_pivot_init_kernel<R>, dim3(nmat), dim3(256), 0, s, b);
   } else if ((stage & 1) == 0) {
@@ -1226,16 +1230,20 @@ void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int sta
                        skip_pivot);
   } else {
     const int k = stage >> 1, nsw = (Tmax + 1) / 2;
-    int gx = wide_tiles(Tmax) - 1;
-    if (b.sched[0]) {  // this sweep's list length (the same schedule the device table holds)
-      static thread_local std::vector<unsigned> tab;
-      static thread_local int tab_T2 = -1;
-      const int T2 = nsw;
-      if (tab_T2 != T2) {
-        wide_schedule(T2, true, tab);
-        tab_T2 = T2;
+    // gx = item slots per factor: the longest list of sweep k over the batch's factors (a factor
+    // with a schedule: its row's length; without one: every lower tile but the pivot's)
+    int gx = 1;
+    for (int m = 0; m < nmat; ++m) {
+      const int T2 = (b.p[m] + WT - 1) / WT;
+      if (k >= T2) continue;
+      int items;
+      if (b.sched[m]) {
+        const std::vector<unsigned>& tab = host_wide_schedule(T2);
+        items = (int)tab[(size_t)k * wide_sched_stride(T2)];
+      } else {
+        items = T2 * (T2 + 1) / 2 - (k + 1 < T2 ? 1 : 0);
       }
-      gx = std::max(1, (int)tab[(size_t)k * wide_sched_stride(T2)]);
+      gx = std::max(gx, items);
     }
     const int per_xcd = (nmat * gx + 7) / 8;
     // persistent tile workgroups: two per CU on all but the 8 CUs whose first-pass workgroup is a
@@ -1248,7 +1256,7 @@ void launch_stage_r(const BigSpdBatch& b, int nmat, int Tmax, int tiles, int sta
                        skip_pivot, gx, per_xcd, nx, fst);
     // after the last sweep of every factor (a smaller factor's last sweep came earlier; later
     // launches leave it alone)
-    if (k + 1 == nsw)
+    if (k + 1 == nsw && mirror)
       hipLaunchKernelGGL(big_mirror_kernel, dim3(Tmax * (Tmax + 1) / 2, nmat), dim3(256), 0, s, b);
   }
 }
@@ -1262,12 +1270,49 @@ size_t spd_big_piv_doubles(int p) { return std::max<size_t>((size_t)p * 32, 2 * 
 
 // stage -1: pivot 0; stage 2k: panel k (standalone; the inverse launches it for k = 0 only);
 // stage 2k+1: update k + the fused panel of sweep k + 1 (profiling / bench)
-hipError_t launch_spd_big_stage(SpdArgs* a, int nmat, int stage, hipStream_t s) {
+hipError_t launch_spd_big_stage(SpdArgs* a, int nmat, int stage, hipStream_t s, bool mirror) {
   int Tmax, tiles;
   BigSpdBatch b = make_batch(a, nmat, Tmax, tiles);
-  if (batch_R(a) == 2) launch_stage_r<2>(b, nmat, Tmax, tiles, stage, s);
-  else launch_stage_r<1>(b, nmat, Tmax, tiles, stage, s);
+  if (batch_R(a) == 2) launch_stage_r<2>(b, nmat, Tmax, tiles, stage, s, 0, mirror);
+  else launch_stage_r<1>(b, nmat, Tmax, tiles, stage, s, 0, mirror);
   return hipGetLastError();
+}
+
+// The MFMA work update launch k (stage 2k + 1) schedules, per the tile lists it walks (bench
+// accounting, gpk_bench_kernel): every listed tile's products, 2 w_I w_J (w_k [+ w_{k-1} for a
+// tile that takes sweeps k - 1 and k]) -- a diagonal tile whole (the kernel keeps both triangles
+// of its block) -- plus, with the pivot workgroup, the next pivot's tile, its blocked Cholesky
+// (W^3 / 3) and the fused next panel (forward substitution, W^2 p).  One-sweep forms: every lower
+// tile of the sweep.  Summed over the launches of one inverse the tile products are p^3 for the
+// one-sweep form (the Gauss-Jordan count).
+double spd_big_update_flops(const SpdArgs* a, int nmat, int k, bool with_pivot) {
+  const int W = batch_R(a) == 2 ? 128 : 64;
+  double fl = 0.0;
+  for (int m = 0; m < nmat; ++m) {
+    const int p = a[m].p, T = (p + W - 1) / W;
+    if (k >= T) continue;
+    auto w = [&](int I) { return (double)std::min(W, p - W * I); };
+    const bool has_next = k + 1 < T;
+    if (W == 128 && a[m].sched) {
+      const std::vector<unsigned>& tab = host_wide_schedule(T);
+      const unsigned* row = tab.data() + (size_t)k * wide_sched_stride(T);
+      auto item = [&](unsigned ent) {
+        const int I = (int)((ent >> 8) & 0xffu), J = (int)(ent & 0xffu);
+        const bool two = (ent >> 16) & 1u;
+        return 2.0 * w(I) * w(J) * (w(k) + (two ? w(k - 1) : 0.0));
+      };
+      for (unsigned i = 0; i < row[0]; ++i) fl += item(row[2 + i]);
+      if (with_pivot && has_next) fl += item(row[1]);
+    } else {
+      for (int I = 0; I < T; ++I)
+        for (int J = 0; J <= I; ++J) {
+          if (!with_pivot && has_next && I == k + 1 && J == k + 1) continue;
+          fl += 2.0 * w(I) * w(J) * w(k);
+        }
+    }
+    if (with_pivot && has_next) fl += w(k + 1) * w(k + 1) * w(k + 1) / 3.0 + w(k + 1) * w(k + 1) * p;
+  }
+  return fl;
 }
 
 // bench: the update launch of sweep k without its pivot workgroup (the tile work alone)

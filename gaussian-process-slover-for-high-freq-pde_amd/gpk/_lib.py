@@ -119,6 +119,7 @@ EXPORTS = {
     "gpk_set_chain_capacity": ([ctypes.c_int32], ctypes.c_int),
     "gpk_set_spd_big_workgroups": ([ctypes.c_int32], ctypes.c_int),
     "gpk_set_wait_limit": ([ctypes.c_int32], ctypes.c_int),
+    "gpk_set_wait_limit_chunk": ([ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
     "gpk_graph_mode": ([ctypes.c_void_p, _ip, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
     "gpk_distance_classes": ([_dp, ctypes.c_int32, _ip, _ip], ctypes.c_int),
     "gpk_class_count": ([ctypes.c_void_p, ctypes.c_int32, _ip], ctypes.c_int),

@@ -316,6 +316,12 @@ def set_wait_limit(polls):
     check(_lib.load().gpk_set_wait_limit(int(polls)))
 
 
+def set_wait_limit_chunk(polls, chunk):
+    """Tests: the poll budget of set_wait_limit, applied only while step() runs its 64-step
+    chunk number `chunk` (0-based); polls = 0 clears it (include/gpk.h)."""
+    check(_lib.load().gpk_set_wait_limit_chunk(int(polls), int(chunk)))
+
+
 def comm_unique_id():
     """128-byte RCCL id for gpk_create_sharded (rank 0 makes it, every rank uses the same)."""
     buf = (ctypes.c_uint8 * 128)()

@@ -189,6 +189,9 @@ int gpk_set_spd_big_workgroups(int32_t workgroups);
  * timed out") and a gpk_step batch is undone (see gpk_step).  Tests force that path with 1 (every
  * wait whose first poll fails gives up). */
 int gpk_set_wait_limit(int32_t polls);
+/* Tests: apply the poll budget only while gpk_step runs chunk `chunk` (0-based, 64-step chunks)
+ * of a later call; polls = 0 clears it. */
+int gpk_set_wait_limit_chunk(int32_t polls, int32_t chunk);
 
 /* Graph selection state (see GPK_FLAG_NO_FAST_GRAPH): *fast = 1 if the next gpk_step uses the
  * fast graph, *rollbacks = batches rerun with the full graph so far.  Either pointer may be NULL. */
@@ -227,10 +230,14 @@ int gpk_loss_grad(gpk_handle* h, double* loss, double* grad_flat);
  * BEFORE each update (as step() returns it); may be NULL.  Returns once the losses and the
  * device status of the call are final: the last step's U update may still be running, like
  * the reference's asynchronously dispatched jax step; every later call on the handle is ordered
- * after it, and gpk_sync waits for it.  A batch (the whole call, or one 64-step chunk of the fast
- * graph) that fails on the device -- GPK_ENOTPD: a non-positive pivot or a hand-off timeout --
- * is undone: params, Adam state and step count are restored from the snapshot the batch took at
- * its start (earlier chunks of the call stay applied, their losses written). */
+ * after it, and gpk_sync waits for it.  Batches: when the handle has a fast graph (every handle
+ * but the row-sharded ones and the large 2D factors), a call is split into 64-step chunks + the
+ * remainder, on the fast and on the full (refining) graph alike, and every chunk is a batch of
+ * its own; otherwise the whole call is one batch.  A batch that fails on the device -- GPK_ENOTPD:
+ * a non-positive pivot or a hand-off timeout -- is undone: params, Adam state and step count are
+ * restored from the snapshot the batch took at its start.  Earlier chunks of the same call stay
+ * applied (their losses are written), so a failed call may have advanced the handle by a
+ * multiple of 64 steps. */
 int gpk_step(gpk_handle* h, int32_t n_steps, double* losses);
 
 /* Wait until every launch enqueued on the handle has finished (timing). */
@@ -276,9 +283,12 @@ int gpk_time_spd_inverse(gpk_handle* h, int32_t iters, double* avg_us);
 
 /* One kernel of the step, launched `iters` times back to back on the handle's stream
  * between two HIP events (after one full step so its inputs are valid; every listed kernel
- * is idempotent).  name: "assemble" | "sweep" | "gemm_B" | "pgrad".  Returns the average
- * device time per launch and the kernel's ALGORITHMIC work per launch (flops, HBM bytes;
- * DESIGN.md §Measurement defines them). */
+ * is idempotent).  name: "assemble" | "sweep" | "gemm_B" | "pgrad" | "spd_chain" | "gather";
+ * large-factor inverse: "sweep" / "spd_tiles" (update launch 0 with / without its pivot
+ * workgroup), "spd_updates" (every update launch of one inverse, averaged per launch),
+ * "spd_pivot" | "spd_panel".  Returns the average device time per launch and the kernel's
+ * ALGORITHMIC work per launch (flops, HBM bytes; DESIGN.md §Measurement defines them; the
+ * large-factor update launches are credited the tile products their lists schedule). */
 int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg_us,
                      double* alg_flops, double* alg_bytes);
 
@@ -289,7 +299,9 @@ int gpk_bench_kernel(gpk_handle* h, const char* name, int32_t iters, double* avg
  * tiles, 3 the 128x128 pipelined tile (model_GP_solver_2d.py:104-119's solves and products
  * are these GEMMs here).  M, N, K, K2 multiples of 32 (the step's padding contract); lda etc.
  * in elements.  iters > 0 times that many back-to-back launches with HIP events after the
- * checked one and returns the average microseconds in *avg_us (may be NULL when iters = 0). */
+ * checked one and returns the average microseconds in *avg_us (may be NULL when iters = 0;
+ * written only on success).  C receives the checked launch's result; with C0 == C the timed
+ * launches keep updating the device copy in place (same work, each on the last one's output). */
 int gpk_dgemm(int32_t variant, int32_t M, int32_t N, int32_t K, double alpha, const double* A,
               int32_t lda, int32_t ta, const double* B, int32_t ldb, int32_t tb, int32_t K2,
               double alpha2, const double* A2, int32_t lda2, int32_t ta2, const double* B2,

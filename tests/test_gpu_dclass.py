@@ -103,21 +103,32 @@ def test_c4_size_class_counts():
 
 
 
-@pytest.mark.parametrize("eq,n1,n2", [("advection", 1056, 64), ("poisson", 1024, 1056)])
-def test_wide_gather_bitwise_class_table(eq, n1, n2):
-    """The large-factor gather (p >= 1024: gather_wide_kernel, class = cbase[|i - j|] + the pair's
-    variant byte) writes exactly the class table's values: K (+ jitter), its kept copy and D
-    (with the advection sign) bitwise equal to the host expansion of (class ids, class values)."""
+@pytest.mark.parametrize("eq,n1,n2,big", [("advection", 1056, 64, True), ("poisson", 1024, 1056, False),
+                                           ("poisson", 2048, 512, False), ("advection", 320, 1664, False)])
+def test_wide_gather_bitwise_class_table(eq, n1, n2, big):
+    """The large-factor gather (max p >= 1024: gather_wide_kernel, class = cbase[|i - j|] + the
+    pair's variant byte) writes exactly the class table's values on EVERY axis, the one below
+    1024 included: K (+ jitter), its kept copy and D (with the advection sign) bitwise equal to
+    the host expansion of (class ids, class values).  (the variant bytes used to be
+    built only for axes with p >= 1024, and the launch returned without assembling anything
+    when one axis lacked them.)"""
+    from gpk._lib import GPK_FLAG_FORCE_BIG_SPD
     prob, params, _, fs = problem_2d(eq=eq, kind="Matern52_Cos_1d", n1=n1, n2=n2, Q=4, seed=5)
-    s = device_solver(prob, 4, fs)
+    s = device_solver(prob, 4, fs, flags=GPK_FLAG_FORCE_BIG_SPD if big else 0)
     try:
         s.set_params(params)
         s.loss_grad()
         for a in (1, 2):
-            n = n1 if a == 1 else n2
-            if n < 1024:
-                continue
-            assert np.array_equal(s.forward_field(f"Kc{a}"), s.forward_field(f"K{a}_classes"))
+            kc, kcls = s.forward_field(f"Kc{a}"), s.forward_field(f"K{a}_classes")
+            assert np.isfinite(kc).all() and np.any(kc != 0)
+            assert np.array_equal(kc, kcls)
             assert np.array_equal(s.forward_field(f"D{a}"), s.forward_field(f"D{a}_classes"))
     finally:
         s.close()
+
+
+def test_wide_gather_unequal_axes_loss_grad():
+    """2048 x 512 (the large-factor path on axis 1; axis 2 below the wide gather's own size):
+    loss and full gradient against the oracle."""
+    prob, params, _, fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=2048, n2=512, Q=4, seed=7)
+    _cmp_lossgrad(prob, params, 4, fs, extended=False)

@@ -231,13 +231,17 @@ def test_big_gemm_adam_and_predict_match_small():
                                                (1, "poisson", "SE_Cos_1d", 330, 0),
                                                (2, "poisson", "Matern52_Cos_1d", 96, 80),
                                                (2, "advection", "SE_Cos_1d", 72, 150),
-                                               (2, "allencahn", "Matern52_1d", 130, 64)])
+                                               (2, "allencahn", "Matern52_1d", 130, 64),
+                                               (2, "poisson", "Matern52_Cos_1d", 300, 600)])
 def test_loss_grad_big_spd_path(dim, eq, kind, n1, n2, wide):
     """The panel/update SPD inverse (spdinv_big.hip, used from p >= 1600: C2, C5), 64-wide and
     128-wide sweeps, forced at small sizes: one-sweep factors (p=64, 96), ragged last pivots
     of 32/64/96 (p=96, 160, 224, 352), the 128-pivot with a 32- or 64-wide second half, a last
     sweep narrower than 64, in-launch pivot hand-off (1 or 3 tiles) over several sweeps, the
-    final mirror and the refinement gate."""
+    final mirror and the refinement gate.  300 x 600 (128-wide: T2 = 3 and 5) gives the two
+    factors schedules of different lengths in one update launch: each factor keeps its own
+    two-sweep table and the launch's item slots cover the longer list (the shorter
+    stride used to null the second factor's schedule and starve its one-sweep tile list)."""
     from gpk._lib import GPK_FLAG_FORCE_BIG_SPD, GPK_FLAG_FORCE_WIDE_SPD, GPK_FLAG_FORCE_NARROW_SPD
     flags = GPK_FLAG_FORCE_BIG_SPD | (GPK_FLAG_FORCE_WIDE_SPD if wide else GPK_FLAG_FORCE_NARROW_SPD)
     if dim == 1:

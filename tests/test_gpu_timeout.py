@@ -150,3 +150,38 @@ def test_group_step_timeout_undone_on_every_rank(wait_limit):
     finally:
         g.close()
         f.close()
+
+
+def test_failure_in_second_chunk_keeps_first_chunk():
+    """A call is split into 64-step batches whenever the handle has a fast graph, on the full
+    (refining) graph too (include/gpk.h gpk_step): a hand-off timeout in the call's SECOND chunk
+    undoes that chunk only -- the handle ends exactly where a handle that ran the first 64 steps
+    alone is (params, Adam state, count), and the first chunk's losses were written."""
+    import ctypes
+    from gpk import _lib
+    from gpk._lib import GPK_ENOTPD
+    from gpk.core import set_wait_limit_chunk
+    prob, params, _, fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=96, n2=80, Q=5, seed=4)
+    s = device_solver(prob, 5, fs)
+    f = device_solver(prob, 5, fs)
+    try:
+        s.set_params(params)
+        f.set_params(params)
+        lf = f.step(64)
+        f.sync()
+        assert not s.graph_mode()[0], "the call must start on the full (refining) graph"
+        set_wait_limit_chunk(1, 1)
+        out = np.full(130, np.nan)
+        try:
+            rc = _lib.load().gpk_step(s._h, 130, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        finally:
+            set_wait_limit_chunk(0, -1)
+        assert rc == GPK_ENOTPD and b"timed out" in _lib.load().gpk_last_error(), rc
+        s.sync()
+        assert _same_state(_state(s), _state(f)), "chunk 0 must stay applied, chunk 1 undone"
+        assert np.array_equal(out[:64], lf)
+        # and the handle goes on as one that never failed
+        assert np.array_equal(s.step(3), f.step(3))
+    finally:
+        s.close()
+        f.close()

@@ -11,7 +11,7 @@ from gpk import problems
 
 s = problems.make_solver("C5", seed=0)
 try:
-    for name in ("spd_pivot", "spd_panel", "spd_tiles", "sweep"):
+    for name in ("spd_pivot", "spd_panel", "spd_tiles", "sweep", "spd_updates"):
         us, fl, by = s.bench_kernel(name, 5)
         print(f"{name:10s} {us:9.2f} us" + (f"  {fl / us / 1e6:.1f} TF/s" if fl else ""), flush=True)
     inv = s.time_spd_inverse(5)
