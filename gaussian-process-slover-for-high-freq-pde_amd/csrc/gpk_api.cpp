@@ -163,6 +163,9 @@ struct gpk_handle {
   std::vector<GemmDesc> sdescs;       // row slices of hdescs
   Stage sst[kGemmStages];
   std::vector<ShardGather> sgather[kGemmStages];
+  // the one per-step all-reduce of a sharded handle: [status (2) | pg | egap | quad] contiguous
+  double* sred = nullptr;
+  std::string splan;                  // the step's shard plan (gpk_shard_plan; gpk/shard.py)
 
   hipGraphExec_t g_exec[2] = {nullptr, nullptr};  // [apply] full step graph
   hipGraphExec_t g_fast[2] = {nullptr, nullptr};  // [apply] without the refinement stages
@@ -311,7 +314,6 @@ static hipError_t launch_inverse(gpk_handle* h, SpdArgs* sa, double** fin, bool 
 }
 
 static int split_broadcast(gpk_handle* h);  // (after ShardComm)
-static int status_allreduce(gpk_handle* h);
 
 // assemble K, D (+ step constants, + pivot block 0) and invert K: the first part of a step
 static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
@@ -940,53 +942,62 @@ static int split_broadcast(gpk_handle* h) {
   return GPK_OK;
 }
 
-// Every sharded step, after the inverse: the device status bits summed over the group.  A
-// non-PD factor under the split is seen only by the ranks that inverted it, and a hand-off
-// timeout (bit 2) is rank-local by nature (one rank's wait gave up); with the bits group-wide
-// every rank fails the batch and undoes it (its snapshot) together -- a rank that carried on
-// would enter the next step's collectives alone and hang, or keep params its peers dropped.
-static int status_allreduce(gpk_handle* h) {
-  TRY(check_launch(launch_status_f64(h->status, h->stat_x, 0, h->s), "status_pack"));
-  TRY(h->comm->allreduce(h, h->stat_x, 2));
-  return check_launch(launch_status_f64(h->status, h->stat_x, 1, h->s), "status_unpack");
-}
-
 // Row slices of the step's GEMM stages for this rank, the variant per stage (its tile rows must
 // divide the slice height so that the per-tile loss partials land in the full-grid slots), and
 // the all-gathers after each stage: exactly the outputs a later stage reads beyond its rows.
+// Every descriptor runs in one of three modes: 'r' its output rows [r h, (r + 1) h) (slice_rows),
+// 'k' this rank's share of its contraction index (slice_k: G_K2, G_D2, summed through the
+// linear parameter contraction) or 'f' whole (replicated on every rank).  The plan -- modes per
+// stage, then the collectives -- is kept as text (gpk_shard_plan) and restated by gpk/shard.py
+// shard_plan(), whose host stand-in runs it across gloo processes (tests/test_shard.py).
+//   augmented chain (small factors, C4): every rank's inverse launch yields the whole A, Bt and
+//   K^{-1} D^T, so the forward refinement (stages 1, 2: the gate's two GEMMs) and X1 =
+//   beta (K1^{-1} D1^T) R with its refinement (stages 6, 8, 9: one P1^3 product each, cheap at
+//   these sizes) run whole: the step's collectives are the R gather, ONE all-reduce and the U
+//   gather.
+//   otherwise (large factors, C5; the factor split): A is gathered after stage 0 and 2 (W1
+//   after the refinement's residual), R, T1 (and X1 / W1 of the reverse refinement) after their
+//   stages -- each a 4096^2 row block exchange instead of a replicated 4096^3 product.
 static int build_shard(gpk_handle* h) {
   const Layout& L = h->L;
   const int P1 = L.p1, P2 = L.p2;
   h->h1 = P1 / h->nranks;
   h->h2 = P2 / h->nranks;
   const int force = gemm_force(h->prob.flags);
+  const bool aug = h->chain_aug;
   h->sdescs.clear();
+  auto mode_of = [&](int k, const GemmDesc& d) -> char {
+    // G_K2 = c N1/2 K2^{-1} - Y2^T Bt and G_D2 = v R^T Bt contract over the P1 rows: each rank
+    // forms the full matrix from its own rows of Y2 / R and Bt (no all-gather of those operands)
+    if (d.C == h->GK[1] || d.C == h->GD[1]) return 'k';
+    if (aug && (k == 1 || k == 2)) return 'f';
+    if (aug && (k == 6 || k == 8 || k == 9) && (d.C == h->X1 || d.C == h->W1)) return 'f';
+    return 'r';
+  };
+  auto slice = [&](char mode, const GemmDesc& d, int variant) {
+    const int rows = d.M == P1 ? h->h1 : h->h2;
+    if (mode == 'k') return slice_k(d, h->rank * h->h1, h->h1, h->rank);
+    if (mode == 'f') return d;
+    return slice_rows(d, h->rank * rows, rows, variant);
+  };
   for (int k = 0; k < kGemmStages; ++k) {
     const GemmDesc* full = h->hdescs.data() + h->st[k].off;
     const int n = h->st[k].n;
     std::vector<GemmDesc> tmp;
-    auto rows_of = [&](const GemmDesc& d) { return d.M == P1 ? h->h1 : h->h2; };
-    // G_K2 = c N1/2 K2^{-1} - Y2^T Bt and G_D2 = v R^T Bt contract over the P1 rows: each rank
-    // forms the full matrix from its own rows of Y2 / R and Bt (no all-gather of those operands)
-    auto ksplit = [&](const GemmDesc& d) { return d.C == h->GK[1] || d.C == h->GD[1]; };
     for (int i = 0; i < n; ++i) {
       const GemmDesc& d = full[i];
       if (d.M != P1 && d.M != P2) return fail(GPK_EINVAL, "shard: unexpected GEMM row count");
-      const int rows = rows_of(d);
-      tmp.push_back(ksplit(d) ? slice_k(d, h->rank * h->h1, h->h1, h->rank)
-                              : slice_rows(d, h->rank * rows, rows, GEMM_SMALL));
+      tmp.push_back(slice(mode_of(k, d), d, GEMM_SMALL));
     }
     int variant = gemm_variant(tmp.data(), n, force);
     for (int i = 0; i < n; ++i)
-      while (!ksplit(full[i]) && rows_of(full[i]) % tile_rows(variant) != 0)
+      while (mode_of(k, full[i]) == 'r' && (full[i].M == P1 ? h->h1 : h->h2) % tile_rows(variant) != 0)
         variant = variant == GEMM_HUGE ? GEMM_BIG : GEMM_SMALL;
     h->sst[k].off = (int)h->sdescs.size();
     h->sst[k].n = n;
     h->sst[k].variant = variant;
     for (int i = 0; i < n; ++i) {
-      const int rows = rows_of(full[i]);
-      h->sdescs.push_back(ksplit(full[i]) ? slice_k(full[i], h->rank * h->h1, h->h1, h->rank)
-                                          : slice_rows(full[i], h->rank * rows, rows, variant));
+      h->sdescs.push_back(slice(mode_of(k, full[i]), full[i], variant));
       if (full[i].red) h->nquad = h->negap = gemm_tiles(full[i], variant);
     }
   }
@@ -996,25 +1007,44 @@ static int build_shard(gpk_handle* h) {
   // rank contracts what it holds and the partials are all-reduced (enqueue_step_shard).
   auto g1 = [&](double* b) { return ShardGather{b, (size_t)h->h1 * P2}; };
   for (auto& v : h->sgather) v.clear();
-  // (the refinement stages this handle has: build_descs, GPK_FLAG_REFINE_ALL / NO_REFINE)
-  if (h->st[1].n > 0) {
-    h->sgather[0] = {g1(h->A)};                                // A_res: K1 A
-    h->sgather[1] = {g1(h->W1)};                               // A_fix: K1^{-1} W1
+  std::string gplan[kGemmStages];
+  auto gather = [&](int k, double* b, const char* name) {
+    h->sgather[k].push_back(g1(b));
+    gplan[k] += std::string(" g") + name;
+  };
+  if (aug) {
+    gather(3, h->R, "R");                                      // X1 = beta P1 R, T = D1^T R (W1)
+  } else {
+    // (the refinement stages this handle has: build_descs, GPK_FLAG_REFINE_ALL / NO_REFINE)
+    if (h->st[1].n > 0) {
+      gather(0, h->A, "A");                                    // A_res: K1 A
+      gather(1, h->W1, "W1");                                  // A_fix: K1^{-1} W1
+    }
+    gather(2, h->A, "A");                                      // R: D1 A;  G_K1 = Y1 A^T
+    gather(3, h->R, "R");                                      // T1 = D1^T R
+    gather(6, h->T1, "T1");                                    // X1 = K1^{-1} T1
+    if (h->st[8].n > 0) {
+      gather(7, h->X1, "X1");                                  // D_res: K1 X1
+      gather(8, h->W1, "W1");                                  // D_fix: K1^{-1} W1
+    }
   }
-  h->sgather[2] = {g1(h->A)};                                  // R: D1 A;  G_K1 = Y1 A^T
-  h->sgather[3] = {g1(h->R)};                                  // T1 = D1^T R
-  h->sgather[6] = {g1(h->T1)};                                 // X1 = K1^{-1} T1
-  if (h->st[8].n > 0) {
-    h->sgather[7] = {g1(h->X1)};                               // D_res: K1 X1
-    h->sgather[8] = {g1(h->W1)};                               // D_fix: K1^{-1} W1
+  // the plan: per stage its descriptors' modes, then the gathers that follow it
+  std::string out;
+  for (int k = 0; k < kGemmStages; ++k) {
+    const GemmDesc* full = h->hdescs.data() + h->st[k].off;
+    if (h->st[k].n) {
+      out += (out.empty() ? "" : " ") + std::string("s") + std::to_string(k) + ":";
+      for (int i = 0; i < h->st[k].n; ++i) out += mode_of(k, full[i]);
+    }
+    out += gplan[k];
   }
+  h->splan = out + " ar gU";  // + the step's one all-reduce and the U rows after Adam
   return GPK_OK;
 }
 
 static int enqueue_step_shard(gpk_handle* h, int apply) {
   const Layout& L = h->L;
   TRY(enqueue_assemble_inverse(h, apply));  // replicated: K, D, K^{-1}, log det, step constants
-  TRY(status_allreduce(h));                  // a failed inverse fails every rank's batch
   for (int k = 0; k < kGemmStages; ++k) {
     if (h->sst[k].n)  // (empty: a refinement stage of a path without refinement)
       TRY(check_launch(launch_gemm_auto(h->sdescs.data() + h->sst[k].off, h->sst[k].n, h->sc, h->s,
@@ -1037,9 +1067,13 @@ static int enqueue_step_shard(gpk_handle* h, int apply) {
   // every rank contracts its own G_K / G_D rows (axis 1) and partials (axis 2) in full
   TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, nullptr), "pgrad"));
   TRY(check_launch(launch_reduce_parts(h->pgpart, h->bpa, 2, L.q, h->pg, h->s), "reduce_parts"));
-  TRY(h->comm->allreduce(h, h->pg, (size_t)2 * 3 * QMAX));
-  TRY(h->comm->allreduce(h, h->red_egap, (size_t)h->negap));
-  TRY(h->comm->allreduce(h, h->red_quad, (size_t)h->nquad));
+  // the step's one all-reduce: [status bits | parameter-contraction partials | per-tile ||R||^2 |
+  // per-tile <A, Bt>], contiguous (h->sred).  The status rides in it: a failed inverse (or a
+  // rank-local hand-off timeout) fails every rank's batch before the loss is formed -- every rank
+  // runs the same collectives whatever its status, so none waits alone
+  TRY(check_launch(launch_status_f64(h->status, h->stat_x, 0, h->s), "status_pack"));
+  TRY(h->comm->allreduce(h, h->sred, (size_t)(h->red_quad + h->nquad - h->sred)));
+  TRY(check_launch(launch_status_f64(h->status, h->stat_x, 1, h->s), "status_unpack"));
   TailArgs T = make_tail(h, apply);
   TRY(check_launch(launch_finalize(T.fin, h->s), "finalize"));
   // this rank's tile slots are rewritten next step; the summed copies must not leak into it
@@ -1466,8 +1500,11 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     const int chains_on_device = in_group ? nranks : 1;
     h->chain = !h->bigspd && h->split_axis < 0 && !(p->flags & GPK_FLAG_NO_CHAIN) &&
                grid_blocks(false) * chains_on_device <= cap;
-    h->chain_aug = h->chain && L.dim == 2 && !shard && !(p->flags & GPK_FLAG_NO_CHAIN_AUG) &&
-                   grid_blocks(true) <= cap;
+    // (row-sharded handles too: the augmented chain gives every rank the whole A, Bt and
+    // K^{-1} D^T from its replicated inverse, so the forward solves need no all-gather -- the
+    // sharded step's plan, build_shard)
+    h->chain_aug = h->chain && L.dim == 2 && !(p->flags & GPK_FLAG_NO_CHAIN_AUG) &&
+                   grid_blocks(true) * chains_on_device <= cap;
     // large 1D factors: the persistent inverse on 64-row macro tiles (chain_multi_kernel), when
     // its grid is co-resident (else the 64/128-wide launch-per-sweep path)
     if (L.dim == 1 && !in_group && h->split_axis < 0 &&
@@ -1566,8 +1603,17 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     if (p->uoff) A_(h->uoff, P1);
     h->nquad = h->negap = gemv_blocks(P1);
   }
-  A_(h->red_quad, h->nquad);
-  A_(h->red_egap, h->negap);
+  if (shard) {  // one all-reduce per sharded step: [status | pg | egap | quad] (enqueue_step_shard)
+    const size_t npg = (size_t)L.naxes * 3 * QMAX;
+    A_(h->sred, 2 + npg + (size_t)h->negap + (size_t)h->nquad);
+    h->stat_x = h->sred;
+    h->pg = h->sred + 2;
+    h->red_egap = h->pg + npg;
+    h->red_quad = h->red_egap + h->negap;
+  } else {
+    A_(h->red_quad, h->nquad);
+    A_(h->red_egap, h->negap);
+  }
   // distance classes (both axes or none), uploaded once: the coordinates never change
   std::vector<double> cdist[2];
   std::vector<int> ccid[2], cbase[2];
@@ -1622,7 +1668,7 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
     h->bpa = std::max(pgrad_blocks(L.n1), L.dim == 2 ? pgrad_blocks(L.n2) : 0);
   }
   A_(h->pgpart, (size_t)L.naxes * h->bpa * 3 * QMAX);
-  A_(h->pg, (size_t)L.naxes * 3 * QMAX);
+  if (!shard) A_(h->pg, (size_t)L.naxes * 3 * QMAX);
   h->ttg = std::max(16, (int)std::ceil(std::sqrt((double)h->bpa)));  // one 16-load batch per level at C4
   h->tngpa = (h->bpa + h->ttg - 1) / h->ttg;
   A_(h->tcount, (size_t)L.naxes * h->tngpa);
@@ -1768,7 +1814,7 @@ static int group_run(gpk_handle** hs, int nranks, int apply, int n_steps) {
   for (auto& t : th) t.join();
   for (int r = 0; r < nranks; ++r)
     if (rcs[r] != GPK_OK) return fail(rcs[r], "rank " + std::to_string(r) + ": " + errs[r]);
-  // every rank's status: the step makes it group-wide (status_allreduce), so ranks that disagree
+  // every rank's status: the step makes it group-wide (its one all-reduce), so ranks that disagree
   // are an internal error.  A failed batch (non-PD factor, or a hand-off timeout: bit 2, raised by
   // one rank's wait and summed over the group) fails the whole group with GPK_ENOTPD; every rank
   // resets its hand-off slots and restores the batch's snapshot.
@@ -1825,6 +1871,14 @@ int gpk_group_loss_grad(gpk_handle** hs, int32_t nranks, double* loss, double* g
                        (size_t)(r1 - r0) * L.n2 * sizeof(double), hipMemcpyDeviceToHost));
     }
   }
+  return GPK_OK;
+}
+
+int gpk_shard_plan(const gpk_handle* h, char* out, int64_t cap) {
+  if (!h || !out || cap < 1) return fail(GPK_EINVAL, "NULL argument");
+  if (!h->shard) return fail(GPK_EINVAL, "gpk_shard_plan: not a row-sharded handle");
+  if ((int64_t)h->splan.size() + 1 > cap) return fail(GPK_EINVAL, "gpk_shard_plan: cap too small");
+  std::memcpy(out, h->splan.c_str(), h->splan.size() + 1);
   return GPK_OK;
 }
 

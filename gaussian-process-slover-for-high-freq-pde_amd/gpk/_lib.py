@@ -115,6 +115,7 @@ EXPORTS = {
     "gpk_group_step": ([ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_int32, _dp], ctypes.c_int),
     "gpk_group_loss_grad": ([ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, _dp, _dp], ctypes.c_int),
     "gpk_shard_info": ([ctypes.c_void_p, _ip, _ip, _ip, _ip], ctypes.c_int),
+    "gpk_shard_plan": ([ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64], ctypes.c_int),
     "gpk_inverse_path": ([ctypes.c_void_p, _ip], ctypes.c_int),
     "gpk_set_chain_capacity": ([ctypes.c_int32], ctypes.c_int),
     "gpk_set_spd_big_workgroups": ([ctypes.c_int32], ctypes.c_int),

@@ -126,6 +126,12 @@ class DeviceSolver:
         check(_lib.load().gpk_shard_info(self._h, *[ctypes.byref(x) for x in v]))
         return tuple(int(x.value) for x in v)
 
+    def shard_plan(self):
+        """The row-sharded step's plan (gpk_shard_plan; gpk/shard.py shard_plan restates it)."""
+        buf = ctypes.create_string_buffer(4096)
+        check(_lib.load().gpk_shard_plan(self._h, buf, len(buf)))
+        return buf.value.decode()
+
     def graph_mode(self):
         """(fast, rollbacks): whether the next step runs the graph without the refinement
         stages, and how many batches were rolled back and rerun with the full graph."""
@@ -368,6 +374,17 @@ class DeviceGroup(DeviceSolver):
         mu, nu = f64(mu).reshape(-1), f64(nu).reshape(-1)
         for k in range(self.nranks):
             check(_lib.load().gpk_set_opt_state(self._hs[k], int(count), dptr(mu), dptr(nu), self.nparams))
+
+    def shard_plan(self, k=0):
+        """Rank k's sharded-step plan (gpk_shard_plan)."""
+        buf = ctypes.create_string_buffer(4096)
+        check(_lib.load().gpk_shard_plan(ctypes.c_void_p(self._hs[k]), buf, len(buf)))
+        return buf.value.decode()
+
+    def inverse_path(self, k=0):
+        v = ctypes.c_int32()
+        check(_lib.load().gpk_inverse_path(ctypes.c_void_p(self._hs[k]), ctypes.byref(v)))
+        return _lib.INV_PATH_NAMES[int(v.value)]
 
     def rank_state(self, k):
         """(flat params, Adam count, mu, nu) held by rank k's handle."""

@@ -45,3 +45,79 @@ def make_sharded_solver(config, ctx, seed=0, Q=30, lr=0.01, flags=0):
     s.set_flat(flat)
     replicas.barrier(ctx)
     return s
+
+
+# ------------------------------------------------------------------------------------------
+# The sharded step's plan (csrc/gpk_api.cpp build_shard; gpk_shard_plan returns the library's)
+# ------------------------------------------------------------------------------------------
+PADM = 32  # padding multiple of a matrix dimension (gpk_api.cpp make_layout), x nranks when sharded
+
+
+def shard_rows(n, nranks, rank):
+    """Rows [r0, r1) of a P-row output that `rank` computes: P = n padded to 32 * nranks, block
+    height P / nranks (the last ranks' blocks may lie in the padding: r0 >= r1)."""
+    m = PADM * nranks
+    p = (n + m - 1) // m * m
+    h = p // nranks
+    r0 = rank * h
+    return min(r0, n), min(n, r0 + h), h
+
+
+def shard_plan(aug, refine_fwd=True, refine_rev=True):
+    """The plan the library builds for a row-sharded 2D handle (gpk_api.cpp build_shard):
+    "s<k>:<modes>" per GEMM stage with products -- r = this rank's output rows, k = its share of
+    the contraction index, f = whole (replicated) -- and " g<buf>" per all-gather after the
+    stage; then "ar" (the step's one all-reduce) and "gU" (U rows after Adam).
+
+    aug: the augmented chain inverse (small factors: A, Bt and K^{-1} D^T whole on every rank);
+    refine_fwd / refine_rev: the gated refinement stages of the forward solves (A, Bt) and of
+    the reverse-pass solves (S, X) are in the graph (build_descs)."""
+    out = []
+
+    def stage(k, modes, gathers=()):
+        if modes:
+            out.append(f"s{k}:{modes}")
+        out.extend(f"g{g}" for g in gathers)
+
+    if not aug:
+        stage(0, "rr", ("A",) if refine_fwd else ())
+    if refine_fwd:
+        stage(1, "ff" if aug else "rr", () if aug else ("W1",))
+        stage(2, "ff" if aug else "rr", () if aug else ("A",))
+    elif not aug:
+        out.append("gA")
+    stage(3, "rr", ("R",))
+    if refine_rev:
+        stage(4, "r")
+        stage(5, "r")
+    stage(6, "frrk" if aug else "rrrk", () if aug else ("T1",))
+    if not aug:
+        stage(7, "rr", ("X1",) if refine_rev else ())
+    if refine_rev:
+        stage(8, "fr" if aug else "rr", () if aug else ("W1",))
+        stage(9, "fr" if aug else "rr")
+    stage(10, "rk")
+    out += ["ar", "gU"]
+    return " ".join(out)
+
+
+def parse_plan(plan):
+    """[(stage, modes, [gathers after it])] + the tail ops, in order: the form a host stand-in
+    executes (tests/shard_standin.py)."""
+    steps = []
+    for tok in plan.split():
+        if tok.startswith("s"):
+            k, modes = tok[1:].split(":")
+            steps.append(("stage", int(k), modes))
+        elif tok.startswith("g"):
+            steps.append(("gather", tok[1:]))
+        elif tok == "ar":
+            steps.append(("allreduce",))
+        else:
+            raise ValueError(f"bad plan token {tok!r}")
+    return steps
+
+
+def plan_collectives(plan):
+    """Collectives per step of a plan (all-gathers + all-reduces)."""
+    return sum(1 for s in parse_plan(plan) if s[0] in ("gather", "allreduce"))

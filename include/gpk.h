@@ -339,6 +339,12 @@ int gpk_group_step(gpk_handle** hs, int32_t nranks, int32_t n_steps, double* los
 int gpk_group_loss_grad(gpk_handle** hs, int32_t nranks, double* loss, double* grad_flat);
 /* this handle's rank, group size and rows [row0, row0 + rows) of U it owns */
 int gpk_shard_info(const gpk_handle* h, int32_t* rank, int32_t* nranks, int32_t* row0, int32_t* rows);
+/* the sharded step's plan as text (NUL-terminated, <= cap bytes): per GEMM stage "s<k>:" and one
+ * mode letter per product -- r = this rank's output rows, k = its share of the contraction
+ * index, f = whole (replicated) -- then " g<buffer>" for each all-gather after that stage; the
+ * step ends with "ar" (its one all-reduce: status, contraction partials, loss partials) and "gU"
+ * (U rows after Adam).  gpk/shard.py shard_plan restates it (tests/test_shard.py). */
+int gpk_shard_plan(const gpk_handle* h, char* out, int64_t cap);
 
 /* ---- 3-axis Kronecker solver (the d > 2 generalisation) ------------
  * The reference's GP_solver_2d_single log joint (model_GP_solver_2d.py:87-183) with

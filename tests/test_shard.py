@@ -15,9 +15,16 @@ import pytest
 from oracle import gp_oracle as O
 from tests.helpers import device_solver, problem_2d, rel
 
-# Sharded handles solve A = K1^{-1} U etc. by GEMMs against K^{-1}; an unsharded handle folds
-# those solves into its inverse launch (GPK_FLAG_NO_CHAIN_AUG) -- compare like with like.
+# A sharded handle whose inverse is the augmented chain (small factors whose grids fit the
+# device) gets A, Bt and K^{-1} D^T from it like an unsharded handle; otherwise it solves them by
+# GEMMs against K^{-1} -- an unsharded handle does that with GPK_FLAG_NO_CHAIN_AUG.  Compare
+# like with like.
 from gpk._lib import GPK_FLAG_NO_CHAIN_AUG as NO_AUG  # noqa: E402
+
+
+def _alg(g):
+    """The unsharded handle's flag that runs the sharded handle g's algorithm."""
+    return 0 if g.inverse_path() == "chain_aug" else NO_AUG
 
 
 def _group(prob, Q, fs, nranks, flags=0):
@@ -44,7 +51,7 @@ def test_group_loss_grad(eq, kind, n1, n2, nranks):
     (unequal axes, ragged last row blocks, padding to 32 * nranks)."""
     prob, params, _, fs = problem_2d(eq=eq, kind=kind, n1=n1, n2=n2, Q=5, seed=21)
     g = _group(prob, 5, fs, nranks)
-    s = device_solver(prob, 5, fs, flags=NO_AUG)  # the sharded step's own algorithm
+    s = device_solver(prob, 5, fs, flags=_alg(g))  # the sharded step's own algorithm
     try:
         g.set_params(params)
         s.set_params(params)
@@ -70,7 +77,7 @@ def test_group_eight_ranks_c4_size():
     prob, params, _, cfg = _config_problem("C4")
     fs = cfg["freq_scale"]
     g = _group(prob, 30, fs, 8)
-    s = device_solver(prob, 30, fs, flags=NO_AUG)
+    s = device_solver(prob, 30, fs, flags=_alg(g))
     try:
         assert g.shard_info()[1] == 8
         g.set_params(params)
@@ -104,9 +111,10 @@ def test_group_chain_path_two_ranks(cid):
     prob, params, _, cfg = _config_problem(cid)
     fs = cfg["freq_scale"]
     g = _group(prob, 30, fs, 2)
-    s = device_solver(prob, 30, fs, flags=NO_AUG)
+    s = device_solver(prob, 30, fs, flags=_alg(g))
     try:
-        assert g.inverse_path() == "chain", g.inverse_path()
+        # (C3: both ranks' augmented chains fit the device together; C4: the plain chain)
+        assert g.inverse_path() == ("chain_aug" if cid == "C3" else "chain"), g.inverse_path()
         assert g.shard_info()[1] == 2
         g.set_params(params)
         s.set_params(params)
@@ -134,7 +142,7 @@ def test_group_trajectory_matches_unsharded(nranks, flags):
     forces the 128x128 GEMM where the row blocks allow it (downgraded per stage otherwise)."""
     prob, params, (Xte, _), fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=200, n2=136, Q=6, seed=3)
     g = _group(prob, 6, fs, nranks, flags=flags)
-    s = device_solver(prob, 6, fs, flags=NO_AUG)
+    s = device_solver(prob, 6, fs, flags=_alg(g))
     try:
         g.set_params(params)
         s.set_params(params)
@@ -247,8 +255,9 @@ def test_rccl_single_rank_sharded_handle():
               logdet=prob["logdet"], lr=0.01, freq_scale=fs)
     r = DeviceSolver(2, prob["eq"], prob["kind"], prob["x1"], prob["src"], prob["bvals"],
                      shard=(0, 1, comm_unique_id()), **kw)
-    s = device_solver(prob, 4, fs, flags=NO_AUG)
+    s = device_solver(prob, 4, fs, flags=0 if r.inverse_path() == "chain_aug" else NO_AUG)
     try:
+        assert r.inverse_path() == "chain_aug"  # (a one-rank RCCL handle: the augmented chain)
         assert r.shard_info() == (0, 1, 0, 64)
         r.set_params(params)
         s.set_params(params)
@@ -297,3 +306,117 @@ def test_comm_id_broadcast_gloo_world2():
         assert p.exitcode == 0
     expect = bytes((7 * i + 3) % 256 for i in range(128))
     assert got[0] == expect and got[1] == expect
+
+
+# ---- the sharded step's plan across processes (CPU, gloo world 2) --------------------------
+def _sharded_section_worker(rank, world, port, q, eq, aug):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import types
+    import bench
+    from gpk import replicas
+    from tests.shard_standin import HostShardedSolver, HostSolver
+    ctx = replicas.init("gloo")
+    try:
+        prob, params, _, _ = problem_2d(eq=eq, kind="Matern52_Cos_1d", n1=40, n2=36, Q=4, seed=11)
+        made = {}
+
+        def make_sharded(cid, flags):
+            made["s"] = HostShardedSolver(prob, params, ctx.world, ctx.rank, aug=aug)
+            return made["s"]
+
+        a = types.SimpleNamespace(sharded_steps=3)
+        out = bench.sharded_section(a, ctx, configs=("C4",), make_sharded=make_sharded,
+                                    make_single=lambda cid: HostSolver(prob, params, aug=aug))
+        s = made["s"]
+        q.put((rank, s.params, s.losses, s.plan, s.collectives_per_step, out["C4"]))
+    finally:
+        replicas.shutdown(ctx)
+
+
+@pytest.mark.parametrize("eq,aug", [("poisson", True), ("allencahn", True), ("advection", True),
+                                    ("poisson", False)])
+def test_sharded_section_gloo_world2_plan(eq, aug):
+    """bench.py's sharded_section over two gloo processes, driving the host stand-in of the
+    sharded step (tests/shard_standin.py): each rank computes only its rows of every product the
+    plan of gpk/shard.py marks 'r' (row partition shard_rows: 40 rows -> 32 + 8), receives the
+    rest only through the plan's all-gathers (rows it neither computed nor received are NaN),
+    and sums its contraction / loss partials in the plan's one all-reduce.  After the section's
+    2 + 3 Adam steps both ranks hold the unsharded oracle trajectory's params; the augmented-chain
+    plan (the small-factor / C4 form) issues 3 collectives per step, the large-factor form 9."""
+    import multiprocessing as mp
+    from gpk.shard import plan_collectives, shard_plan
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sharded_section_worker, args=(r, 2, port, q, eq, aug)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict((r[0], r[1:]) for r in (q.get(timeout=300) for _ in ps))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    prob, params, _, _ = problem_2d(eq=eq, kind="Matern52_Cos_1d", n1=40, n2=36, Q=4, seed=11)
+    # (explicit inverses against the oracle's LU solves: the cond(K) budget of the parity tests)
+    tol = max(1e-9, _tol(prob, params))
+    opt = O.Adam(0.01)
+    st = opt.init(params)
+    ref_losses = []
+    for _ in range(5):
+        lo, go = O.loss_grad_2d(prob, params)
+        ref_losses.append(lo)
+        params, st = opt.update(go, st, params)
+    plan = shard_plan(aug)
+    for r in (0, 1):
+        p_r, losses, plan_r, ncoll, entry = got[r]
+        assert plan_r == plan
+        assert ncoll == plan_collectives(plan) == (3 if aug else 9)
+        assert np.isfinite(losses).all()
+        assert rel(np.asarray(losses), np.asarray(ref_losses)) < tol
+        assert rel(O.flatten_params(p_r), O.flatten_params(params)) < tol
+        assert entry["ranks"] == 2 and entry["steps"] == 3 and entry["speedup_vs_1gpu"] > 0
+    assert np.array_equal(O.flatten_params(got[0][0]), O.flatten_params(got[1][0]))
+
+
+def test_shard_plan_missing_gather_poisons():
+    """The stand-in detects a plan that lacks an all-gather a later product needs: without the
+    R gather the reverse pass reads rows this rank never computed (NaN) and the gradient is
+    poisoned -- the check the gloo test relies on."""
+    from tests.shard_standin import HostShardedSolver
+
+    class Local:  # two ranks' exchange emulated in one process is not needed: rank 0 of 2, no peers
+        count = 0
+
+        def gather_rows(self, M, h):
+            self.count += 1
+            return M
+
+        def allreduce(self, v):
+            self.count += 1
+            return v
+
+    prob, params, _, _ = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=40, n2=36, Q=4, seed=11)
+    s = HostShardedSolver(prob, params, 2, 0, aug=True, exchange=Local())
+    s.steps = [op for op in s.steps if op != ("gather", "R")]
+    _, grad = s._loss_grad()
+    assert not np.isfinite(O.flatten_params(grad)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags_name,aug", [(None, True), ("GPK_FLAG_NO_CHAIN_AUG", False),
+                                            ("GPK_FLAG_FORCE_BIG_SPD", False)])
+def test_library_shard_plan_matches_gpk_shard(flags_name, aug):
+    """The library's sharded step (gpk_shard_plan of every rank of an in-process group) is the
+    plan gpk/shard.py restates and the gloo stand-in test executes."""
+    from gpk import _lib
+    from gpk.shard import shard_plan
+    flags = getattr(_lib, flags_name) if flags_name else 0
+    prob, params, _, fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=72, n2=64, Q=4, seed=8)
+    g = _group(prob, 4, fs, 2, flags=flags)
+    try:
+        assert (g.inverse_path() == "chain_aug") == aug, g.inverse_path()
+        big = flags_name == "GPK_FLAG_FORCE_BIG_SPD"
+        for k in range(2):
+            assert g.shard_plan(k) == shard_plan(aug, True, not big), g.shard_plan(k)
+    finally:
+        g.close()

@@ -15,7 +15,7 @@ tests/helpers.rel).  With --fixture it writes tests/golden/ext_<config>.npz: the
 and the LU oracle's own distance per key -- what the GPU parity tests measure the device against
 (tests/test_gpu_accuracy.py).
 
-usage: python tools/solve_accuracy.py C2 [C4 C5 ...] [--fixture] [--no-inv]
+usage: python tools/solve_accuracy.py C2 [C4 C5 T3072 ...] [--fixture] [--no-inv]
 C5 (two 4096 factors, 7 long-double solves with 4096 right-hand sides) takes ~4 minutes on 8 cores.
 """
 import argparse
@@ -30,8 +30,12 @@ import numpy as np
 import scipy.linalg as sla
 
 from oracle import gp_oracle as O
-from tests.helpers import config_problem, rel
+from tests.helpers import config_problem, problem_2d, rel
 
+# GPU tests' own problems with a yardstick fixture: T3072 is tests/test_gpu_fullsize.py's
+# 3072^2 advection case (the 128x128-tile GEMM stages vs the 64x64 kernel, both checked against
+# the yardstick instead of against each other)
+TEST_PROBLEMS = {"T3072": dict(eq="advection", kind="Matern52_Cos_1d", n1=3072, n2=3072, Q=6, seed=3)}
 SAMPLE = 16384          # dL/dU elements kept in a fixture when the field is larger than 2^20
 SAMPLE_SEED = 1234
 
@@ -92,7 +96,10 @@ def main():
     O.set_backend(True)
     report = {}
     for cid in a.configs:
-        prob, params, _, cfg = config_problem(cid)
+        if cid in TEST_PROBLEMS:  # a GPU test's own problem (not a BASELINE config)
+            prob, params, _, _ = problem_2d(**TEST_PROBLEMS[cid])
+        else:
+            prob, params, _, cfg = config_problem(cid)
         res = {}
         for mode in ["lu", "ext"] + ([] if a.no_inv else ["inv"]):
             t = time.time()
