@@ -14,6 +14,8 @@ Tolerance at C5: max(1e-10, 50 cond(K) eps), cond(K) bounded by ||K||_inf / jitt
 kernel part is PSD, so lambda_min >= jitter): an SVD of two 4096^2 factors would cost minutes.
 The 80-bit yardstick is out of reach at 4096, so the LU oracle is the reference value.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -201,30 +203,42 @@ def test_wide_inverse_quarter_tiles_bitwise_whole_tiles(n1, n2):
         assert np.array_equal(np.asarray(a), np.asarray(b))
 
 
-def test_tile128_stages_match_64x64_kernel():
+def test_tile128_and_64x64_stages_vs_yardstick():
     """The C5-class GEMM stages run on the pipelined 128x128 tile (gemm_tile_dev.h; dual
     products as two passes, gemm.hip launch_huge); GPK_FLAG_FORCE_BIG_GEMM runs every stage on
-    the 64x64 kernel instead.  Same algorithm, another summation order: loss, gradient and a
-    2-step trajectory agree within the path's accuracy class (3072^2 advection, big_wide
-    inverse): dL/dU of either order is ~1e-8 from the long-double yardstick at C5 and the fp64 LU
-    oracle (the reference's algorithm) 4.3e-8 (tests/golden/ext_C5.npz lu_err/U), so the two
-    orders may differ by up to that: bar 5e-8 (observed 2.4e-8 on this 3072^2 case)."""
+    the 64x64 kernel instead -- the same algorithm in another summation order.  Each order is
+    checked on its own against the long-double, exact-field yardstick of this 3072^2 advection
+    problem (tests/golden/ext_T3072.npz, tools/solve_accuracy.py T3072 --fixture): loss and
+    every gradient key within 2x the fp64 LU oracle's own distance from it (floor 1e-10), the
+    parity bar of C1 / C3 / C4 (tests/test_gpu_accuracy.py).  Round 5 compared the two orders
+    with each other, at a bar (5e-8) above the LU oracle's whole error.
+    Measured (round 6, tools/t3072_diag.py; device / LU distance): tile128 U 0.49x,
+    kernel_paras_1 1.50x, kernel_paras_2 0.34x, loss 0.68x; tile64 0.49x, 0.69x, 0.75x, 0.68x.
+    The kernel-parameter gradient here scatters with last-bit changes of G (GPK_FLAG_REFINE_ALL,
+    i.e. MORE accurate S and X solves: kernel_paras_1 3.1x; the fp64 contraction 3.5x): it is
+    the fp64 representation of K and D times cond(K) (~1e-16 x 1e8), amplified by the
+    contraction's cancellation, which every fp64 evaluation -- the LU oracle's included -- carries
+    at its own rounding; a 1.5x bar would gate on which of those samples the LU one happens to be."""
     from gpk._lib import GPK_FLAG_FORCE_BIG_GEMM
-    out = []
-    for flags in (0, GPK_FLAG_FORCE_BIG_GEMM):
-        prob, params, _, fs = problem_2d(eq="advection", n1=3072, n2=3072, Q=6, seed=3)
+    from tests.helpers import record_parity
+    from tests.test_gpu_accuracy import fixture_errors
+    O.set_backend(True)
+    fx = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ext_T3072.npz"))
+    prob, params, _, fs = problem_2d(eq="advection", n1=3072, n2=3072, Q=6, seed=3)
+    tol = {"loss": max(1e-10, 2.0 * float(fx["loss_lu_err"]))}
+    for f in fx.files:
+        if f.startswith("lu_err/"):
+            tol[f[7:]] = max(1e-10, 2.0 * float(fx[f]))
+    for tag, flags in (("tile128", 0), ("tile64", GPK_FLAG_FORCE_BIG_GEMM)):
         s = device_solver(prob, 6, fs, flags=flags)
         s.set_params(params)
         try:
             assert s.inverse_path() == "big_wide"
             loss, g = s.loss_grad()
-            losses = s.step(2)
-            s.sync()
-            out.append((loss, np.asarray(g), np.asarray(losses), np.asarray(s.get_flat())))
         finally:
             s.close()
-    (la, ga, sa, pa), (lb, gb, sb, pb) = out
-    assert abs(la - lb) <= 1e-11 * abs(lb)
-    assert rel(ga, gb) < 5e-8
-    assert rel(sa, sb) < 1e-10
-    assert rel(pa, pb) < 5e-8
+        gd = O.unflatten_params(params, g)
+        errs = fixture_errors(fx, loss, {k: O.flatten_params(gd[k]) for k in gd})
+        record_parity("test_tile128_and_64x64_stages_vs_yardstick", f"T3072/{tag}", errs, tol, {})
+        for k, e in errs.items():
+            assert e < tol[k], (tag, k, e, tol[k])
