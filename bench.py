@@ -196,6 +196,7 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split"), make_sharded=None,
     make_sharded(cid, flags) / make_single(cid): solver factories (the dry run passes stand-ins,
     so the launcher tests run this very code on CPU)."""
     from gpk import replicas
+    from gpk.shard import plan_collectives
     if make_sharded is None:
         from gpk import shard
         from gpk._lib import GPK_FLAG_SPLIT_FACTORS
@@ -212,6 +213,7 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split"), make_sharded=None,
         steps = a.sharded_steps if cid == "C4" else max(2, a.sharded_steps // 10)
         STAGE["name"] = f"sharded {key}: create"
         s = make_sharded(cid, flags)
+        plan = s.shard_plan() if hasattr(s, "shard_plan") else None
         try:
             STAGE["name"] = f"sharded {key}: prepare + warm-up"
             s.prepare(steps)
@@ -228,12 +230,15 @@ def sharded_section(a, ctx, configs=("C4", "C5", "C5_split"), make_sharded=None,
             s.close()
         dt = replicas.max_over_ranks(t1 - t0, ctx)
         out[key] = {"value": steps / dt, "unit": "iters/s", "ms_per_step": dt / steps * 1e3,
-                    "steps": steps, "ranks": ctx.world}
+                    "steps": steps, "ranks": ctx.world, "plan": plan,
+                    "collectives_per_step": None if plan is None else plan_collectives(plan)}
         if cid not in single:
             STAGE["name"] = f"sharded {key}: single-GPU reference on rank 0"
             single[cid] = single_gpu_reference(lambda: make_single(cid), steps, ctx)
         out[key].update(single[cid])
         out[key]["speedup_vs_1gpu"] = single[cid]["single_gpu_ms_per_step"] / out[key]["ms_per_step"]
+        STAGE["name"] = f"sharded {key}: collective latency"
+        out[key]["ceiling"] = strong_scaling_ceiling(out[key], collective_latency_us(ctx, cid), ctx.world)
     # C5 is reported both ways: both factors inverted on every rank, or one factor
     # per rank half + a broadcast of K^{-1}; the default is the replicated form
     out["C5_default"] = "C5 (replicated inverse); C5_split = GPK_FLAG_SPLIT_FACTORS"
@@ -248,7 +253,7 @@ def single_gpu_reference(make, steps, ctx):
     barrier): ms per step of `steps` timed steps after a prepared warm-up, the denominator of a
     sharded entry's speedup_vs_1gpu (strong scaling, measured in the same run)."""
     from gpk import replicas
-    ms = None
+    ms, rep = None, None
     if ctx.rank == 0:
         s = make()
         try:
@@ -259,12 +264,70 @@ def single_gpu_reference(make, steps, ctx):
             s.step(steps)
             s.sync()
             ms = (time.perf_counter() - t0) / steps * 1e3
+            if hasattr(s, "profile_stages"):
+                # the part of the step every rank repeats in a sharded run: assembly + the SPD
+                # inverse of both factors (+ the step constants), HIP events per stage
+                st = s.profile_stages(3)
+                rep = sum(st.get(k, 0.0) for k in ("prep", "assemble", "spd_inverse")) / 1e3
         finally:
             s.close()
     # every rank gets rank 0's time (the others contribute 0 to the MAX): each rank computes the
     # same speedup and leaves the section together
     ms = replicas.max_over_ranks(ms if ms is not None else 0.0, ctx)
-    return {"single_gpu_ms_per_step": ms, "single_gpu_steps": steps}
+    rep = replicas.max_over_ranks(rep if rep is not None else -1.0, ctx)
+    return {"single_gpu_ms_per_step": ms, "single_gpu_steps": steps,
+            "single_gpu_replicated_ms": rep if rep >= 0.0 else None}
+
+
+def collective_latency_us(ctx, cid, iters=20):
+    """The price of one of the sharded step's collectives on this group, measured here: an
+    all-gather of the config's row block (h rows x P columns of fp64 per rank: the R / U
+    gathers) and an all-reduce of the step's reduction vector size, torch.distributed on the
+    same devices and backend (RCCL over xGMI on GPU ranks), average of `iters` after a warm-up."""
+    from gpk import replicas
+    if ctx.world == 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    from gpk.problems import CONFIGS
+    n = CONFIGS[cid]["n"]
+    m = 32 * ctx.world
+    p = (n + m - 1) // m * m
+    dev = f"cuda:{ctx.local}" if ctx.backend == "nccl" else "cpu"
+    blk = torch.zeros(p // ctx.world * p, dtype=torch.float64, device=dev)
+    parts = [torch.empty_like(blk) for _ in range(ctx.world)]
+    red = torch.zeros(2 + 6 * 64 + 2 * (p // 16) ** 2, dtype=torch.float64, device=dev)
+
+    def timed(fn):
+        fn()
+        if dev != "cpu":
+            torch.cuda.synchronize()
+        replicas.barrier(ctx)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        if dev != "cpu":
+            torch.cuda.synchronize()
+        return replicas.max_over_ranks((time.perf_counter() - t0) / iters * 1e6, ctx)
+    return {"allgather_us": timed(lambda: dist.all_gather(parts, blk)),
+            "allreduce_us": timed(lambda: dist.all_reduce(red)),
+            "allgather_bytes_per_rank": blk.numel() * 8}
+
+
+def strong_scaling_ceiling(entry, lat, world):
+    """A-priori strong-scaling bound of a sharded entry from measured pieces: T_N >= T_rep +
+    (T_1 - T_rep) / N + gathers x t_allgather + t_allreduce, where T_rep (assembly + SPD
+    inverse, single GPU) is repeated on every rank and the rest of the 1-GPU step divides
+    perfectly over N ranks."""
+    t1, rep, plan = entry.get("single_gpu_ms_per_step"), entry.get("single_gpu_replicated_ms"), entry.get("plan")
+    if not t1 or rep is None or plan is None or lat is None:
+        return None
+    ngather = sum(1 for tok in plan.split() if tok.startswith("g"))
+    coll_ms = (ngather * lat["allgather_us"] + lat["allreduce_us"]) / 1e3
+    tn = rep + (t1 - rep) / world + coll_ms
+    return {"replicated_ms": rep, "parallel_ms_per_rank": (t1 - rep) / world, "gathers": ngather,
+            "allreduces": 1, "collectives_ms": coll_ms, **lat, "ms_per_step_bound": tn,
+            "speedup_ceiling": t1 / tn}
 
 
 def dry_run_sharded_section(a, ctx):

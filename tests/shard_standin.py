@@ -217,6 +217,9 @@ class HostShardedSolver:
         return loss
 
     # -- the solver interface bench.py's sharded_section drives ----------------------------
+    def shard_plan(self):
+        return self.plan
+
     def prepare(self, n):
         pass
 
