@@ -267,6 +267,7 @@ static void fill_spd(gpk_handle* h, SpdArgs* sa) {
     sa[a].flag = h->aflag[a];
     sa[a].wide = h->bigwide ? 1 : 0;
     sa[a].no_quarters = (h->prob.flags & GPK_FLAG_NO_QUARTER_TILES) ? 1 : 0;
+    sa[a].qfirst = (h->prob.flags & GPK_FLAG_NO_QUARTER_FIRST) ? 0 : 1;
     sa[a].Z = h->Zp[a];
     sa[a].sched = h->wsched[a];
   }

@@ -221,6 +221,7 @@ struct SpdArgs {
   unsigned int* flag;  // large path: [3] hand-off / pivot-done / panel-row counters
   int wide;        // large path: 128-wide sweeps (else 64)
   int no_quarters; // 128-wide update: keep the last round in whole tiles (tests, GPK_FLAG_NO_QUARTER_TILES)
+  int qfirst;      // 128-wide update: quarter items before whole tiles (GPK_FLAG_NO_QUARTER_FIRST: after)
   double* Z;       // large path: panel buffers [3][128][p] by sweep mod 3 (nullable: Y)
   // 128-wide update schedule (wide_schedule): per sweep, the tiles the launch updates and the
   // sweeps (1 or 2) each applies; null: every tile every sweep (the one-sweep form)

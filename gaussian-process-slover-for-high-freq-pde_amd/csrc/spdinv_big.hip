@@ -67,6 +67,7 @@ struct BigSpdBatch {
   int G;                 // tile workgroups per factor in the update launch
   int nmat;
   int no_quarters;       // (SpdArgs::no_quarters)
+  int qfirst;            // (SpdArgs::qfirst)
   const unsigned* sched[2];  // 128-wide update schedule (wide_schedule) per factor, row stride sstride[m]
   int sstride[2];
 };
@@ -798,6 +799,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   const bool quarters = !b.no_quarters && full_rounds >= 1 && rem_tiles > 0 && 4 * rem_tiles <= nx;
   // item j of this workgroup -> (factor m, tile ti, tj, quarter qq: -1 = whole tile); false past
   // its run
+  bool skip_q = false;  // (the quarter item was worked first: quarter_first below)
   auto tile_at = [&](int j, int& m, int& ti, int& tj, int& qq, unsigned& ent) -> bool {
     qq = -1;
     ent = 0u;
@@ -813,7 +815,7 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     int loc;
     if (quarters && j >= full_rounds) {
       const int w = tt >> 3;
-      if (j > full_rounds || w >= 4 * rem_tiles) return false;
+      if (skip_q || j > full_rounds || w >= 4 * rem_tiles) return false;
       loc = full_rounds * nx + (w >> 2);
       qq = w & 3;
     } else {
@@ -851,114 +853,10 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
   double* sB0 = sm + 2 * SZ;
   int m, ti, tj, qq;
   unsigned ent;
-  if (!tile_at(0, m, ti, tj, qq, ent)) return;
-  int j = 0;
-  for (; qq < 0; ++j) {
-    if (probe && !pivot && j < 2) {  // (trace build) round-0/1 phases over every tile workgroup
-      TR_LO(SLOT_BIG_R0START + 3 * j);
-      TR_HI(SLOT_BIG_R0START + 3 * j);
-    }
-    const int p = b.p[m];
-    const int T2 = (p + WT - 1) / WT;  // 128-tiles per dimension
-    const bool has_next = k + 1 < T2;
-    const bool LAST = !has_next;  // (per factor: the factors of a batch may differ in size)
-    const int Q = k + 1;
-    double* X = b.X[m];
-    const double* Z = zbuf<2>(b, m, k);
-    const int i0 = WT * ti, j0 = WT * tj;
-    const int wK = min(WT, p - WT * k);  // sweep width (a multiple of 32)
-    const bool inPi = ti == k, inPj = tj == k;
-    const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
-    // the workgroup's next item
-    int m2 = 0, ti2 = 0, tj2 = 0, q2 = -1;
-    unsigned ent2 = 0u;
-    const bool next = tile_at(j + 1, m2, ti2, tj2, q2, ent2);
-    // The accumulators start at the tile's current values NEGATED (zero base in the swept blocks;
-    // clamped addresses: rows / columns past p are never stored) and the product is added; the
-    // store negates back: base - Z_I^T Z_J with the rounding of a subtraction (round-to-nearest
-    // commutes with negation), and no separate base registers.  The base loads are issued ahead
-    // of the product loop's first K-step.
-    // Two-sweep schedule (b.sched): new = c0 X + c1 Z_{k-1}^T Z_{k-1} + c2 Z_k^T Z_k, the
-    // coefficients (0, +-1) composing the sweeps' rules (wide_schedule); the products scale the
-    // A operand by c1 / c2 (exact).  One sweep (c1 = 0): the same operations as the form below,
-    // negated throughout -- bitwise the same values.  Without a schedule: the accumulators start
-    // at the tile NEGATED (zero base in the swept blocks) and the store negates back.
-    const bool sch = b.sched[m] != nullptr;
-    const bool two = sch && ((ent >> 16) & 1u);
-    auto cf = [](unsigned c) { return c == 0u ? 0.0 : c == 1u ? 1.0 : -1.0; };
-    const double c0 = cf((ent >> 18) & 3u), c1 = cf((ent >> 20) & 3u), c2 = cf((ent >> 22) & 3u);
-    d4 acc[4][4];
-    {
-      const double f = sch ? c0 : ((inPi || inPj) ? -0.0 : -1.0);
-#pragma unroll
-      for (int bx = 0; bx < 4; ++bx)
-#pragma unroll
-        for (int by = 0; by < 4; ++by)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = min(i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r, p - 1);
-            const int col = min(j0 + 64 * wc + 16 * by + (lane & 15), p - 1);
-            acc[bx][by][r] = X[(size_t)row * p + col] * f;
-          }
-    }
-    // acc += Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j]) -- both
-    // mn-contiguous, staged [k][mn] without a transpose (tile::product<1, 0>)
-    // (one call for every case -- a second inlined product loop spilled the accumulators: two
-    // sweeps read panel k - 1, always 128 deep since it is not the last sweep, then panel k)
-    {
-      const double* Zp = two ? zbuf<2>(b, m, k - 1) : Z;
-      tile::product2<1, 0>(Zp, Zp, two ? WT : 0, c1, Z, Z, wK, sch ? c2 : 1.0, p, p, p, p, i0, j0, sm, t,
-                           wr, wc, lane, acc);
-    }
-    if (probe && !pivot && j < 2) TR_HI(SLOT_BIG_R0START + 3 * j + 2);
-    double mx = 0.0;
-#pragma unroll
-    for (int bx = 0; bx < 4; ++bx) {
-#pragma unroll
-      for (int by = 0; by < 4; ++by)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r;
-          const int col = j0 + 64 * wc + 16 * by + (lane & 15);
-          if (row < p && col < p) {
-            const double v = sch ? acc[bx][by][r] : -sgn * acc[bx][by][r];
-            X[(size_t)row * p + col] = v;
-            if (LAST && row == col && row < b.n[m]) mx = fmax(mx, v);
-          }
-        }
-      asm volatile("" ::: "memory");
-    }
-    if (LAST && ti == tj) {  // refinement gate: max_i (K^{-1})_ii
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-      if (lane == 0 && mx > 0.0)
-        atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
-                  (unsigned long long)__double_as_longlong(mx));
-    }
-    if (pivot) {
-      // the next pivot block, factored in place from this workgroup's own stores (one L1 per
-      // workgroup: visible after the barrier)
-      if (probe && m == 0) TR_HI(SLOT_BIG_PIVTILE);
-      __syncthreads();
-      const int r0 = WT * Q, w = min(WT, p - r0);
-      pivot_blk<2>(X + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 4 * Q, b.status[m], sm);
-      release_add(b.flag[m] + 1, 1u);  // L^{-1} of pivot k + 1 ready (fused_panel)
-      if (probe && m == 0) TR_HI(SLOT_BIG_PIVOT);
-      return;
-    }
-    if (probe && j < 2) TR_HI(SLOT_BIG_ROUND0 + j);
-    if (has_next && (ti == Q || tj == Q)) release_add(b.flag[m] + 2, 4u);  // next panel row
-    if (!next) return;
-    m = m2;
-    ti = ti2;
-    tj = tj2;
-    qq = q2;
-    ent = ent2;
-  }
   // the quarter item (qq = 2 qi + qj): rows WT ti + 64 qi, columns WT tj + 64 qj; this wave's
   // 32 x 32 block (wr, wc) as 2 x 2 MFMA blocks, 16-deep K-steps through the same double-buffered
   // staging ([k][64] rows of Z at stride S)
-  {
+  auto quarter_item = [&]() {
     __syncthreads();  // (the whole-tile loop's last reads of the staging buffers)
     if (probe) TR_LO(SLOT_BIG_QUARTER);
     const int p = b.p[m];
@@ -1073,7 +971,130 @@ __global__ __launch_bounds__(256, 2) void wide_update_kernel(BigSpdBatch b, int 
     }
     if (has_next && (ti == Q || tj == Q)) release_add(b.flag[m] + 2, 1u);  // a quarter of a row tile
     if (probe) TR_HI(SLOT_BIG_QUARTER);
+  };
+  // Quarter items first (round 6): on most CUs one of the two tile workgroups has a quarter item
+  // besides its whole tiles and the other has none; working the quarter FIRST puts the two
+  // workgroups' memory phases (base loads, stores) out of step, so one runs its product loop while
+  // the other waits on memory, instead of both bursting together.  Not for a workgroup whose first
+  // whole tile is in the next panel's row / column (eager: the fused panel waits for those).
+  // Every item is computed the same way in either order (bitwise).
+  if (quarters && !pivot && !b.no_quarters && (tt >> 3) < 4 * rem_tiles && b.qfirst) {
+    bool eager = true;
+    if (tile_at(0, m, ti, tj, qq, ent)) {
+      const int T2 = (b.p[m] + WT - 1) / WT;
+      eager = k + 1 < T2 && (ti == k + 1 || tj == k + 1);
+    }
+    if (!eager && tile_at(full_rounds, m, ti, tj, qq, ent) && qq >= 0) {
+      quarter_item();
+      skip_q = true;
+      __syncthreads();  // (its staging reads before the whole tiles' first stores)
+    }
   }
+  if (!tile_at(0, m, ti, tj, qq, ent)) return;
+  int j = 0;
+  for (; qq < 0; ++j) {
+    if (probe && !pivot && j < 2) {  // (trace build) round-0/1 phases over every tile workgroup
+      TR_LO(SLOT_BIG_R0START + 3 * j);
+      TR_HI(SLOT_BIG_R0START + 3 * j);
+    }
+    const int p = b.p[m];
+    const int T2 = (p + WT - 1) / WT;  // 128-tiles per dimension
+    const bool has_next = k + 1 < T2;
+    const bool LAST = !has_next;  // (per factor: the factors of a batch may differ in size)
+    const int Q = k + 1;
+    double* X = b.X[m];
+    const double* Z = zbuf<2>(b, m, k);
+    const int i0 = WT * ti, j0 = WT * tj;
+    const int wK = min(WT, p - WT * k);  // sweep width (a multiple of 32)
+    const bool inPi = ti == k, inPj = tj == k;
+    const double sgn = ((inPi != inPj) ? -1.0 : 1.0) * (LAST ? -1.0 : 1.0);
+    // the workgroup's next item
+    int m2 = 0, ti2 = 0, tj2 = 0, q2 = -1;
+    unsigned ent2 = 0u;
+    const bool next = tile_at(j + 1, m2, ti2, tj2, q2, ent2);
+    // The accumulators start at the tile's current values NEGATED (zero base in the swept blocks;
+    // clamped addresses: rows / columns past p are never stored) and the product is added; the
+    // store negates back: base - Z_I^T Z_J with the rounding of a subtraction (round-to-nearest
+    // commutes with negation), and no separate base registers.  The base loads are issued ahead
+    // of the product loop's first K-step.
+    // Two-sweep schedule (b.sched): new = c0 X + c1 Z_{k-1}^T Z_{k-1} + c2 Z_k^T Z_k, the
+    // coefficients (0, +-1) composing the sweeps' rules (wide_schedule); the products scale the
+    // A operand by c1 / c2 (exact).  One sweep (c1 = 0): the same operations as the form below,
+    // negated throughout -- bitwise the same values.  Without a schedule: the accumulators start
+    // at the tile NEGATED (zero base in the swept blocks) and the store negates back.
+    const bool sch = b.sched[m] != nullptr;
+    const bool two = sch && ((ent >> 16) & 1u);
+    auto cf = [](unsigned c) { return c == 0u ? 0.0 : c == 1u ? 1.0 : -1.0; };
+    const double c0 = cf((ent >> 18) & 3u), c1 = cf((ent >> 20) & 3u), c2 = cf((ent >> 22) & 3u);
+    d4 acc[4][4];
+    {
+      const double f = sch ? c0 : ((inPi || inPj) ? -0.0 : -1.0);
+#pragma unroll
+      for (int bx = 0; bx < 4; ++bx)
+#pragma unroll
+        for (int by = 0; by < 4; ++by)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = min(i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r, p - 1);
+            const int col = min(j0 + 64 * wc + 16 * by + (lane & 15), p - 1);
+            acc[bx][by][r] = X[(size_t)row * p + col] * f;
+          }
+    }
+    // acc += Z_I^T Z_J: op(A) = Z^T (Z[k][i], i contiguous), op(B) = Z (Z[k][j]) -- both
+    // mn-contiguous, staged [k][mn] without a transpose (tile::product<1, 0>)
+    // (one call for every case -- a second inlined product loop spilled the accumulators: two
+    // sweeps read panel k - 1, always 128 deep since it is not the last sweep, then panel k)
+    {
+      const double* Zp = two ? zbuf<2>(b, m, k - 1) : Z;
+      tile::product2<1, 0>(Zp, Zp, two ? WT : 0, c1, Z, Z, wK, sch ? c2 : 1.0, p, p, p, p, i0, j0, sm, t,
+                           wr, wc, lane, acc);
+    }
+    if (probe && !pivot && j < 2) TR_HI(SLOT_BIG_R0START + 3 * j + 2);
+    double mx = 0.0;
+#pragma unroll
+    for (int bx = 0; bx < 4; ++bx) {
+#pragma unroll
+      for (int by = 0; by < 4; ++by)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i0 + 64 * wr + 16 * bx + (lane >> 4) + 4 * r;
+          const int col = j0 + 64 * wc + 16 * by + (lane & 15);
+          if (row < p && col < p) {
+            const double v = sch ? acc[bx][by][r] : -sgn * acc[bx][by][r];
+            X[(size_t)row * p + col] = v;
+            if (LAST && row == col && row < b.n[m]) mx = fmax(mx, v);
+          }
+        }
+      asm volatile("" ::: "memory");
+    }
+    if (LAST && ti == tj) {  // refinement gate: max_i (K^{-1})_ii
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+      if (lane == 0 && mx > 0.0)
+        atomicMax(reinterpret_cast<unsigned long long*>(b.pst[m] + 1),
+                  (unsigned long long)__double_as_longlong(mx));
+    }
+    if (pivot) {
+      // the next pivot block, factored in place from this workgroup's own stores (one L1 per
+      // workgroup: visible after the barrier)
+      if (probe && m == 0) TR_HI(SLOT_BIG_PIVTILE);
+      __syncthreads();
+      const int r0 = WT * Q, w = min(WT, p - r0);
+      pivot_blk<2>(X + (size_t)r0 * p + r0, p, w, b.Li[m], b.ldet[m] + 4 * Q, b.status[m], sm);
+      release_add(b.flag[m] + 1, 1u);  // L^{-1} of pivot k + 1 ready (fused_panel)
+      if (probe && m == 0) TR_HI(SLOT_BIG_PIVOT);
+      return;
+    }
+    if (probe && j < 2) TR_HI(SLOT_BIG_ROUND0 + j);
+    if (has_next && (ti == Q || tj == Q)) release_add(b.flag[m] + 2, 4u);  // next panel row
+    if (!next) return;
+    m = m2;
+    ti = ti2;
+    tj = tj2;
+    qq = q2;
+    ent = ent2;
+  }
+  quarter_item();
 }
 
 // After the last 128-wide sweep: upper 64x64 tiles outside the diagonal 128 blocks <- the
@@ -1192,6 +1213,7 @@ BigSpdBatch make_batch(SpdArgs* a, int nmat, int& Tmax, int& tiles_max) {
   b.G = g_big_wgs.load() > 0 ? g_big_wgs.load() : 255;
   b.nmat = nmat;
   b.no_quarters = a[0].no_quarters;
+  b.qfirst = a[0].qfirst;
   for (int m = 0; m < nmat; ++m) {
     // every factor keeps its own schedule (built for its own T2 = ceil(p / 128)); the update
     // launch's per-factor item count covers the longest list (launch_stage_r)

@@ -137,6 +137,10 @@ typedef struct gpk_problem {
 /* 128-wide SPD inverse (factors >= 3072): every lower tile takes every sweep in its own pass
  * (default: tiles take sweeps in pairs, K = 256 per pass, half the tiles per launch). */
 #define GPK_FLAG_ONE_SWEEP_UPDATE 524288
+/* 128-wide SPD inverse: a tile workgroup with a quarter item works it after its whole tiles
+ * (default: first, unless its first whole tile is in the next panel's row / column; A/B only).
+ * Bitwise the same results. */
+#define GPK_FLAG_NO_QUARTER_FIRST 1048576
 
 typedef struct gpk_handle gpk_handle;
 
