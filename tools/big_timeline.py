@@ -17,9 +17,13 @@ NAMES = {240: "launch start (wg 0)", 241: "pivot wg: start .. its tile done", 24
          252: "round 1: first K-step done (last wg)", 253: "round 1: K-loop done (last wg)"}
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--flags", default="0", help="problem flags: an int or GPK_FLAG_* names joined by |")
 a = ap.parse_args()
+flags = 0
+for f in a.flags.split("|"):
+    flags |= int(f) if f.strip().isdigit() else getattr(_lib, f.strip())
 lib = _lib.load()
-s = problems.make_solver("C5", seed=0)
+s = problems.make_solver("C5", seed=0, flags=flags)
 rows = []
 try:
     s.loss_grad()
@@ -35,7 +39,7 @@ try:
                          (hi[k] - t0) / 100.0 if hi[k] else np.nan) for k in NAMES})
 finally:
     s.close()
-print(f"C5 wide update launch, sweep 8, factor 0 (us from the launch's first workgroup; mean of {a.reps})")
+print(f"C5 wide update launch, sweep 8, factor 0, flags {a.flags} (us from the launch's first workgroup; mean of {a.reps})")
 for k, nm in NAMES.items():
     l = np.nanmean([r[k][0] for r in rows]) if any(np.isfinite(r[k][0]) for r in rows) else np.nan
     h = np.nanmean([r[k][1] for r in rows]) if any(np.isfinite(r[k][1]) for r in rows) else np.nan
