@@ -602,6 +602,15 @@ static int build_descs(gpk_handle* h) {
   const int rfl = h->prob.flags;
   const bool ref_fwd = !(rfl & GPK_FLAG_NO_REFINE);
   const bool ref_rev = (!h->bigspd || (rfl & GPK_FLAG_REFINE_ALL)) && !(rfl & GPK_FLAG_NO_REFINE);
+  // Large 2D factors, the axis-2 forward solve Bt = U K2^{-1} (round 6): it enters the residual
+  // R = beta D1 A + Bt D2^T - F with weight 1 against beta for A, so at beta >= 16 (advection;
+  // C5: beta = 200) refining A alone leaves R's error ~1/beta of the unrefined one.  Measured at
+  // C5 against the exact-field yardstick (tools/c5_refine_diag.py, profiles/r6_c5_refine_fwd1.txt):
+  // log_v (||R||^2) 3.3e-12 with A refined alone, 1.1e-12 with both, 8.3e-9 with neither (the LU
+  // oracle: 2.9e-10); every other key within 0.3x of the LU oracle's distance either way -- and
+  // the step 37.3 -> 33.5 ms (two 4096^3 products fewer).  GPK_FLAG_REFINE_ALL refines both.
+  const bool ref_fwd2 = ref_fwd && !(rfl & GPK_FLAG_REFINE_FWD1_ONLY) &&
+                        (!h->bigspd || beta < 16.0 || (rfl & GPK_FLAG_REFINE_ALL));
   bool ref_now = ref_fwd;
   auto pushg = [&](const GemmDesc& g) {
     if (ref_now) d.push_back(g);
@@ -630,7 +639,7 @@ static int build_descs(gpk_handle* h) {
     pushg(gate(g, 0));
     GemmDesc g2 = mk(h->Bt, P2, 0, h->Kc[1], P2, 0, h->W2, P2, P1, P2, P2);
     g2.alpha = -1.0; g2.beta = 1.0; g2.C0 = h->Up; g2.ldc0 = P2;
-    pushg(gate(g2, 1));
+    if (ref_fwd2) pushg(gate(g2, 1));
   }
   end(1);
   begin(2);  // A += K1^{-1} W1, Bt += W2 K2^{-1}  (in place)
@@ -640,7 +649,7 @@ static int build_descs(gpk_handle* h) {
     pushg(gate(g, 0));
     GemmDesc g2 = mk(h->W2, P2, 0, h->Kinv[1], P2, 0, h->Bt, P2, P1, P2, P2);
     g2.beta = 1.0; g2.C0 = h->Bt; g2.ldc0 = P2;
-    pushg(gate(g2, 1));
+    if (ref_fwd2) pushg(gate(g2, 1));
   }
   end(2);
   // Stage B: S = A K2^{-1};  R = beta D1 A + Bt D2^T - F (+AC), ||R||^2 and the prior's

@@ -33,6 +33,7 @@ GPK_FLAG_DD_CONTRACTION = 131072
 GPK_FLAG_NO_DD_CONTRACTION = 262144
 GPK_FLAG_ONE_SWEEP_UPDATE = 524288
 GPK_FLAG_NO_QUARTER_FIRST = 1048576
+GPK_FLAG_REFINE_FWD1_ONLY = 2097152
 GPK_INV_SWEEP, GPK_INV_CHAIN, GPK_INV_CHAIN_AUG, GPK_INV_BIG, GPK_INV_BIG_WIDE, GPK_INV_CHAIN_MULTI = range(6)
 INV_PATH_NAMES = {0: "sweep", 1: "chain", 2: "chain_aug", 3: "big", 4: "big_wide", 5: "chain_multi"}
 KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}

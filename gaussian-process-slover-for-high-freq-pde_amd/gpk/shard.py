@@ -63,7 +63,7 @@ def shard_rows(n, nranks, rank):
     return min(r0, n), min(n, r0 + h), h
 
 
-def shard_plan(aug, refine_fwd=True, refine_rev=True):
+def shard_plan(aug, refine_fwd=True, refine_rev=True, refine_fwd2=True):
     """The plan the library builds for a row-sharded 2D handle (gpk_api.cpp build_shard):
     "s<k>:<modes>" per GEMM stage with products -- r = this rank's output rows, k = its share of
     the contraction index, f = whole (replicated) -- and " g<buf>" per all-gather after the
@@ -71,7 +71,8 @@ def shard_plan(aug, refine_fwd=True, refine_rev=True):
 
     aug: the augmented chain inverse (small factors: A, Bt and K^{-1} D^T whole on every rank);
     refine_fwd / refine_rev: the gated refinement stages of the forward solves (A, Bt) and of
-    the reverse-pass solves (S, X) are in the graph (build_descs)."""
+    the reverse-pass solves (S, X) are in the graph (build_descs); refine_fwd2: Bt's forward
+    refinement too (large factors at beta >= 16 -- advection, C5 -- refine A alone)."""
     out = []
 
     def stage(k, modes, gathers=()):
@@ -82,8 +83,9 @@ def shard_plan(aug, refine_fwd=True, refine_rev=True):
     if not aug:
         stage(0, "rr", ("A",) if refine_fwd else ())
     if refine_fwd:
-        stage(1, "ff" if aug else "rr", () if aug else ("W1",))
-        stage(2, "ff" if aug else "rr", () if aug else ("A",))
+        m = ("f" if aug else "r") * (2 if refine_fwd2 else 1)
+        stage(1, m, () if aug else ("W1",))
+        stage(2, m, () if aug else ("A",))
     elif not aug:
         out.append("gA")
     stage(3, "rr", ("R",))

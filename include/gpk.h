@@ -141,6 +141,9 @@ typedef struct gpk_problem {
  * (default: first, unless its first whole tile is in the next panel's row / column; A/B only).
  * Bitwise the same results. */
 #define GPK_FLAG_NO_QUARTER_FIRST 1048576
+/* Large 2D factors: refine only the axis-1 forward solve A = K1^{-1} U (not Bt = U K2^{-1}), as
+ * the default does when beta >= 16 (advection); diagnostics (tools/c5_refine_diag.py). */
+#define GPK_FLAG_REFINE_FWD1_ONLY 2097152
 
 typedef struct gpk_handle gpk_handle;
 

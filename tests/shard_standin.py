@@ -56,7 +56,7 @@ class GlooExchange:
 
 class HostShardedSolver:
     def __init__(self, prob, params, world, rank, aug=True, refine_fwd=True, refine_rev=True,
-                 lr=0.01, exchange=None):
+                 lr=0.01, exchange=None, refine_fwd2=True):
         self.prob = prob
         self.params = {k: (dict(v) if isinstance(v, dict) else np.array(v, dtype=np.float64))
                        for k, v in params.items()}
@@ -64,7 +64,8 @@ class HostShardedSolver:
         self.state = self.opt.init(self.params)
         self.world, self.rank = world, rank
         self.x = exchange or GlooExchange(world, rank)
-        self.plan = SH.shard_plan(aug, refine_fwd, refine_rev)
+        self.plan = SH.shard_plan(aug, refine_fwd, refine_rev, refine_fwd2)
+        self.fwd2 = refine_fwd2
         self.steps = SH.parse_plan(self.plan)
         self.aug = aug
         N1 = len(prob["x1"])
@@ -117,9 +118,11 @@ class HostShardedSolver:
             if k == 0:
                 return [("A", lambda: K1i @ B["U"]), ("Bt", lambda: B["U"] @ K2i)]
             if k == 1:
-                return [("W1", lambda: B["U"] - K1 @ B["A"]), ("W2", lambda: B["U"] - B["Bt"] @ K2)]
+                return [("W1", lambda: B["U"] - K1 @ B["A"])] + \
+                    ([("W2", lambda: B["U"] - B["Bt"] @ K2)] if self.fwd2 else [])
             if k == 2:
-                return [("A", lambda: B["A"] + K1i @ B["W1"]), ("Bt", lambda: B["Bt"] + B["W2"] @ K2i)]
+                return [("A", lambda: B["A"] + K1i @ B["W1"])] + \
+                    ([("Bt", lambda: B["Bt"] + B["W2"] @ K2i)] if self.fwd2 else [])
             if k == 3:
                 def resid():
                     R = beta * (D1 @ B["A"]) + B["Bt"] @ D2.T - F

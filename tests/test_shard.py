@@ -309,7 +309,7 @@ def test_comm_id_broadcast_gloo_world2():
 
 
 # ---- the sharded step's plan across processes (CPU, gloo world 2) --------------------------
-def _sharded_section_worker(rank, world, port, q, eq, aug):
+def _sharded_section_worker(rank, world, port, q, eq, aug, fwd2=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import types
@@ -322,34 +322,36 @@ def _sharded_section_worker(rank, world, port, q, eq, aug):
         made = {}
 
         def make_sharded(cid, flags):
-            made["s"] = HostShardedSolver(prob, params, ctx.world, ctx.rank, aug=aug)
+            made["s"] = HostShardedSolver(prob, params, ctx.world, ctx.rank, aug=aug, refine_fwd2=fwd2)
             return made["s"]
 
         a = types.SimpleNamespace(sharded_steps=3)
         out = bench.sharded_section(a, ctx, configs=("C4",), make_sharded=make_sharded,
-                                    make_single=lambda cid: HostSolver(prob, params, aug=aug))
+                                    make_single=lambda cid: HostSolver(prob, params, aug=aug, refine_fwd2=fwd2))
         s = made["s"]
         q.put((rank, s.params, s.losses, s.plan, s.collectives_per_step, out["C4"]))
     finally:
         replicas.shutdown(ctx)
 
 
-@pytest.mark.parametrize("eq,aug", [("poisson", True), ("allencahn", True), ("advection", True),
-                                    ("poisson", False)])
-def test_sharded_section_gloo_world2_plan(eq, aug):
+@pytest.mark.parametrize("eq,aug,fwd2", [("poisson", True, True), ("allencahn", True, True),
+                                         ("advection", True, True), ("poisson", False, True),
+                                         ("advection", False, False)])
+def test_sharded_section_gloo_world2_plan(eq, aug, fwd2):
     """bench.py's sharded_section over two gloo processes, driving the host stand-in of the
     sharded step (tests/shard_standin.py): each rank computes only its rows of every product the
     plan of gpk/shard.py marks 'r' (row partition shard_rows: 40 rows -> 32 + 8), receives the
     rest only through the plan's all-gathers (rows it neither computed nor received are NaN),
     and sums its contraction / loss partials in the plan's one all-reduce.  After the section's
     2 + 3 Adam steps both ranks hold the unsharded oracle trajectory's params; the augmented-chain
-    plan (the small-factor / C4 form) issues 3 collectives per step, the large-factor form 9."""
+    plan (the small-factor / C4 form) issues 3 collectives per step, the large-factor form 9 (7
+    with the large advection factors' forward refinement of A alone, the C5 form)."""
     import multiprocessing as mp
     from gpk.shard import plan_collectives, shard_plan
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_sharded_section_worker, args=(r, 2, port, q, eq, aug)) for r in range(2)]
+    ps = [ctx.Process(target=_sharded_section_worker, args=(r, 2, port, q, eq, aug, fwd2)) for r in range(2)]
     for p in ps:
         p.start()
     got = dict((r[0], r[1:]) for r in (q.get(timeout=300) for _ in ps))
@@ -366,7 +368,7 @@ def test_sharded_section_gloo_world2_plan(eq, aug):
         lo, go = O.loss_grad_2d(prob, params)
         ref_losses.append(lo)
         params, st = opt.update(go, st, params)
-    plan = shard_plan(aug)
+    plan = shard_plan(aug, refine_fwd2=fwd2)
     for r in (0, 1):
         p_r, losses, plan_r, ncoll, entry = got[r]
         assert plan_r == plan
@@ -403,20 +405,24 @@ def test_shard_plan_missing_gather_poisons():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags_name,aug", [(None, True), ("GPK_FLAG_NO_CHAIN_AUG", False),
-                                            ("GPK_FLAG_FORCE_BIG_SPD", False)])
-def test_library_shard_plan_matches_gpk_shard(flags_name, aug):
+@pytest.mark.parametrize("eq,flags_name,aug", [("poisson", None, True), ("poisson", "GPK_FLAG_NO_CHAIN_AUG", False),
+                                               ("poisson", "GPK_FLAG_FORCE_BIG_SPD", False),
+                                               ("advection", "GPK_FLAG_FORCE_BIG_SPD", False)])
+def test_library_shard_plan_matches_gpk_shard(eq, flags_name, aug):
     """The library's sharded step (gpk_shard_plan of every rank of an in-process group) is the
     plan gpk/shard.py restates and the gloo stand-in test executes."""
     from gpk import _lib
     from gpk.shard import shard_plan
     flags = getattr(_lib, flags_name) if flags_name else 0
-    prob, params, _, fs = problem_2d(eq="poisson", kind="Matern52_Cos_1d", n1=72, n2=64, Q=4, seed=8)
+    prob, params, _, fs = problem_2d(eq=eq, kind="Matern52_Cos_1d", n1=72, n2=64, Q=4, seed=8)
     g = _group(prob, 4, fs, 2, flags=flags)
     try:
         assert (g.inverse_path() == "chain_aug") == aug, g.inverse_path()
         big = flags_name == "GPK_FLAG_FORCE_BIG_SPD"
+        # (large factors: no reverse refinement; advection's beta = 200 >= 16: A's forward
+        # refinement alone)
+        fwd2 = not (big and eq == "advection")
         for k in range(2):
-            assert g.shard_plan(k) == shard_plan(aug, True, not big), g.shard_plan(k)
+            assert g.shard_plan(k) == shard_plan(aug, True, not big, fwd2), g.shard_plan(k)
     finally:
         g.close()
