@@ -347,6 +347,25 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
   // wave wv runs the epilogue of the tile's rows lane / 16 + 4 wv (one output per lane): its
   // operands are prefetched now so their latency hides under the MFMAs
   const EpiIn ein = epi_fetch(d, i0 + (lane >> 4) + 4 * wv, j0 + (lane & 15));
+  // class partials (d.cpart): this lane's element's class id and, for thread t < CB_SLOTS =
+  // (signed diagonal offset dl, variants v = t & 7 and v + 8), the class range of its diagonal
+  // -- all fixed by the tile's position, so loaded here with the epilogue operands (loads only:
+  // arithmetic on the loaded values here made the compiler wait for them before the operand
+  // loads, a whole memory round trip per launch -- epi_fetch's rule)
+  int bu = -1, bcb = 0, bc0 = 0, bc1 = 0;
+  double bxi = 0.0, bxj = 0.0;
+  if (d.cpart) {  // (uniform)
+    const int row = i0 + (lane >> 4) + 4 * wv, col = j0 + (lane & 15);
+    bu = d.bcid[(size_t)row * d.ldc + col];
+    bcb = d.bcbase[min(abs(row - col), d.bn)];
+    if (d.bsx) {
+      bxi = d.bsx[min(row, d.bn - 1)];
+      bxj = d.bsx[min(col, d.bn - 1)];
+    }
+    const int k = min(abs(16 * ((i0 - j0) >> 4) + (t >> 3) - 15), d.bn - 1);
+    bc0 = d.bcbase[k];
+    bc1 = d.bcbase[k + 1];
+  }
   if (!open) return;  // uniform
   int b0, b1, c0 = 0, c1 = 0;
   range(d.K, b0, b1);
@@ -377,7 +396,7 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
   if (d.vscale) alpha *= sc->v;
   if (d.vscale2) alpha2 *= sc->v;
   const double vv = d.Y ? sc->v : 0.0;
-  double red = 0.0, red2 = 0.0;
+  double red = 0.0, red2 = 0.0, cval;
   {
     const int q = lane * 4 + wv;
     const double s1 = (part[0][0][q] + part[0][1][q]) + (part[0][2][q] + part[0][3][q]);
@@ -387,6 +406,60 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
     c = epi_apply(d, c, ein, red, red2);
     d.C[(size_t)row * d.ldc + col] = c;
     epi_side(d, row, col, c, ein, vv);
+    cval = c;
+  }
+  if (d.cpart) {  // (uniform) the tile's sums per (signed diagonal, variant), rows in order
+    // the tile in LDS diagonal-major: element (r, c) at [r - c + 15][r], so the thread of
+    // diagonal offset dl reads its row of 16 with 16-byte loads (8 threads of one diagonal share
+    // it: a broadcast); positions off the diagonal's range are masked by r, never read as data
+    double* bv = smem + 2 * 4 * 256 + 512;                 // [31][16] values
+    int* bvar = reinterpret_cast<int*>(bv + 31 * 16);      // [31][16] variants
+    {
+      const int r = (lane >> 4) + 4 * wv, c = lane & 15, e = (r - c + 15) * 16 + r;
+      bv[e] = (d.bsx && !(bxi - bxj >= 0.0)) ? -cval : cval;  // D_x1: s_ij G_D (JAX abs'(0) = +1)
+      bvar[e] = bu >= 0 ? bu - bcb : -1;
+    }
+    __syncthreads();
+    // this thread's slots: class (k, v) [and (k, v + 8)] at (sign, band group, tile row)
+    const int dl = (t >> 3) - 15, v = t & 7;
+    int bslot = -1, bslot2 = -1;
+    {
+      const int I = i0 >> 4, b = I - (j0 >> 4), s = 16 * b + dl, k = abs(s);
+      const int fb = s >= 0 ? s / 16 : -((15 - s) / 16);  // floor(s / 16)
+      const int e = ((s < 0 ? 2 : 0) + (b == fb ? 0 : 1)) * tn + I - max(0, b);
+      if (t < CB_SLOTS && k < d.bn) {
+        if (v < bc1 - bc0) bslot = e * d.bncls + bc0 + v;
+        if (v + 8 < bc1 - bc0) bslot2 = e * d.bncls + bc0 + v + 8;
+      }
+    }
+    if (bslot >= 0) {  // (bslot2 >= 0 only if bslot is)
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      typedef int i4v __attribute__((ext_vector_type(4)));
+      const d2v* rv = reinterpret_cast<const d2v*>(bv + (dl + 15) * 16);
+      const i4v* rw = reinterpret_cast<const i4v*>(bvar + (dl + 15) * 16);
+      double x[16];
+      int w[16];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const d2v a = rv[q];
+        x[2 * q] = a.x;
+        x[2 * q + 1] = a.y;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const i4v a = rw[q];
+        w[4 * q] = a.x; w[4 * q + 1] = a.y; w[4 * q + 2] = a.z; w[4 * q + 3] = a.w;
+      }
+      double s = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool in = (unsigned)(r - dl) < 16u;  // column r - dl inside the tile
+        if (in && w[r] == v) s += x[r];
+        if (in && w[r] == v + 8) s2 += x[r];
+      }
+      d.cpart[bslot] = s;
+      if (bslot2 >= 0) d.cpart[bslot2] = s2;
+    }
   }
   if (d.red || d.red2) {  // (uniform) the tile's partials: waves' terms in row order, then lanes
     double* sred = smem + 2 * 4 * 256;  // (past `part`, which other waves may still be reading)

@@ -115,6 +115,10 @@ struct gpk_handle {
          *X1 = nullptr, *X2 = nullptr, *W1 = nullptr, *W2 = nullptr;  // W: refinement residuals
   double *Y1 = nullptr, *Y2 = nullptr;  // S/2 + v X1, S/2 + v X2 (the G_K operands)
   double *GK[2] = {}, *GD[2] = {};
+  // 2D class path: class tile partials of G_K / G_D written by their GEMM epilogues
+  // ([class_slots(P/16)][ncls] per axis; GemmDesc::cpart); cp_on: the stages use them
+  double *cpK[2] = {}, *cpD[2] = {};
+  bool cp_on = false;
   // 1D work
   double *alpha = nullptr, *tvec = nullptr, *beta = nullptr;
   double *red_quad = nullptr, *red_egap = nullptr;
@@ -471,6 +475,11 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
       pa[a].part = h->pgpart + (size_t)a * h->bpa * 3 * QMAX;
       pa[a].part_lo = h->pg_dd ? h->pgpart_lo + (size_t)a * h->bpa * 3 * QMAX : nullptr;
       pa[a].cls = h->cls[a];
+      if (h->cp_on) {
+        pa[a].cpK = h->cpK[a];
+        pa[a].cpD = h->cpD[a];
+        pa[a].cslots = class_slots(pa[a].p / 16);
+      }
     }
     TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, &tail), "pgrad"));
@@ -754,6 +763,23 @@ static int build_descs(gpk_handle* h) {
     d.push_back(g2);
   }
   end(10);
+  // class tile partials (GemmDesc::cpart) from the G_D (stage C) and G_K (stage E) epilogues
+  // when both stages run the 16x16-tile kernel (its epilogue forms them)
+  h->cp_on = h->cpK[0] && h->st[6].variant == GEMM_SMALL && h->st[10].variant == GEMM_SMALL;
+  if (h->cp_on) {
+    for (int k : {6, 10})
+      for (int i = h->st[k].off; i < h->st[k].off + h->st[k].n; ++i)
+        for (int a = 0; a < 2; ++a) {
+          GemmDesc& g = d[i];
+          if (g.C != (k == 6 ? h->GD[a] : h->GK[a])) continue;
+          g.cpart = k == 6 ? h->cpD[a] : h->cpK[a];
+          g.bcid = h->cls[a].cid;
+          g.bcbase = h->cls[a].cbase;
+          g.bn = a == 0 ? n1 : n2;
+          g.bncls = h->cls[a].ncls;
+          g.bsx = (k == 6 && h->prob.eq == GPK_ADVECTION) ? (a == 0 ? h->x1 : h->x2) : nullptr;
+        }
+  }
   {  // the residual descriptor of stage B carries the egap / quad partials: one per tile
     int nq = 0;
     for (int i = h->st[3].off; i < h->st[3].off + h->st[3].n; ++i)
@@ -1673,6 +1699,16 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
       }
     }
     h->bpa = std::max(pgrad_class_blocks(h->cls[0].ncls), L.dim == 2 ? pgrad_class_blocks(h->cls[1].ncls) : 0);
+    // 2D, <= CB_VMAX variants per diagonal, unsharded: the G_K / G_D GEMMs sum their tiles per
+    // class (build_descs turns it on when both stages take the 16x16-tile kernel)
+    if (L.dim == 2 && !shard && !(p->flags & GPK_FLAG_NO_CLASS_BINS) && vmax[0] <= CB_VMAX &&
+        vmax[1] <= CB_VMAX) {
+      for (int a = 0; a < 2; ++a) {
+        const size_t ns = (size_t)h->cls[a].ncls * class_slots((a == 0 ? P1 : P2) / 16);
+        A_(h->cpK[a], ns);
+        A_(h->cpD[a], ns);
+      }
+    }
     h->cls_gemv = h->chain_multi && L.dim == 1 && !(p->flags & GPK_FLAG_MATRIX_GEMV);
   } else {
     h->bpa = std::max(pgrad_blocks(L.n1), L.dim == 2 ? pgrad_blocks(L.n2) : 0);
@@ -2259,6 +2295,12 @@ int gpk_distance_classes(const double* x, int32_t n, int32_t* ncls, int32_t* vma
 int gpk_class_count(const gpk_handle* h, int32_t axis, int32_t* ncls) {
   if (!h || !ncls || axis < 0 || axis >= h->L.naxes) return fail(GPK_EINVAL, "bad argument");
   *ncls = h->cls[axis].ncls;
+  return GPK_OK;
+}
+
+int gpk_class_sum_path(const gpk_handle* h, int32_t* epilogue) {
+  if (!h || !epilogue) return fail(GPK_EINVAL, "bad argument");
+  *epilogue = h->cp_on ? 1 : 0;
   return GPK_OK;
 }
 

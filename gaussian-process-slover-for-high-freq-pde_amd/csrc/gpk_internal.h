@@ -377,7 +377,25 @@ struct GemmDesc {
   // 128x128-tile kernel only: a partial product added to alpha op(A) op(B) before the epilogue
   // (the first pass of a dual product, launch_gemm_auto's split)
   const double* Cp; int ldcp;
+  // 16x16-tile kernel only: class sums of the stored G_K / G_D (cpart != nullptr; see
+  // class_slots below).  bcid / bcbase: the axis' ClassArgs cid (leading dimension ldc) and
+  // cbase, bn its true size; bsx (nullable): coordinates for the D_x1 sign s_ij
+  double* cpart; const int* bcid; const int* bcbase; const double* bsx; int bn, bncls;
 };
+// Class tile partials (GemmDesc::cpart, round 6): the G_K / G_D producers sum their 16x16
+// output tile per (signed diagonal, distance variant) and store each sum into the slot of its
+// class, so the contraction adds per class class_slots(T) partials (T = 16x16 tiles per side)
+// instead of a class-sum launch's chunk partials.  Diagonal s = i - j of class (k, v) lies in
+// tile band b = I - J with |s - 16 b| <= 15: b = floor(s/16) (group 0) or floor(s/16) + 1
+// (group 1); slot e = (sign(s) < 0, group, I - max(0, b)).  Layout [e][class]: a tile's slots
+// for its ~31 consecutive diagonals are consecutive classes (whole-line stores), and the
+// contraction's 16 consecutive classes per slot are one line.  Slots no tile maps to stay zero
+// (allocated zeroed, never written).
+__host__ __device__ inline int class_slots(int T) { return 4 * T; }
+// epilogue threads: (signed diagonal offset in a 16x16 tile, variant v < 8 -- and v + 8: the
+// epilogue handles diagonals of up to 16 variants; C4's grid has 9)
+constexpr int CB_SLOTS = 31 * 8;
+constexpr int CB_VMAX = 16;
 constexpr int GEMM_MAX_BATCH = 4;
 struct GemmBatch {  // passed by value (kernarg): no dependent descriptor load before the operands
   GemmDesc d[GEMM_MAX_BATCH];
@@ -441,6 +459,9 @@ struct PGradArgs {
   // double-double; part holds the partials' high parts, part_lo their low parts (null: fp64)
   double* part_lo;
   ClassArgs cls;                          // ncls > 0: class sums + per-class contraction
+  // 2D class path: the G_K / G_D GEMM epilogues wrote class tile partials ([cslots][ncls],
+  // GemmDesc::cpart) -- no class-sum launch, the contraction adds each class's slots in order
+  const double* cpK; const double* cpD; int cslots;
 };
 struct TailArgs;  // stepk.h
 // tail (nullable): the fused step tail carried by the same launch (stepk.h TailArgs)

@@ -453,11 +453,17 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
     const int ul = t & (PG_CLS - 1), cs = t / PG_CLS;  // 16 chunk slices
     const int u = blk * PG_CLS + ul;
     double sk = 0.0, sdd = 0.0;
-    if (u < C.ncls)
+    if (u < C.ncls && A.cpK) {  // the GEMM epilogues' class tile partials (class_slots)
+      for (int e = cs; e < A.cslots; e += 256 / PG_CLS) {
+        sk += A.cpK[(size_t)e * C.ncls + u];
+        sdd += A.cpD[(size_t)e * C.ncls + u];
+      }
+    } else if (u < C.ncls) {
       for (int c = cs; c < C.nchunk; c += 256 / PG_CLS) {
         sk += C.part[(size_t)c * C.ncls + u];
         sdd += C.part[(size_t)(C.nchunk + c) * C.ncls + u];
       }
+    }
     sacc[cs >> 1][0][(cs & 1) * PG_CLS + ul] = sk;  // scratch: [16 slices][16 classes] x 2
     sacc[cs >> 1][1][(cs & 1) * PG_CLS + ul] = sdd;
     __syncthreads();
@@ -675,8 +681,11 @@ static void launch_pg_t(const PGradBatch& b, int naxes, int bpa, int q, int deri
       vmax = std::max(vmax, b.ax[k].cls.vmax);
       nchunk = std::max(nchunk, b.ax[k].cls.nchunk);
     }
-    if (vmax <= 8) launch_csum_v<8>(b, nchunk, nbands, deriv, mode1d, sc, s);
-    else launch_csum_lds(b, nchunk, nbands, deriv, mode1d, vmax, sc, s);
+    // (class tile partials from the G_K / G_D GEMMs: no class-sum launch)
+    if (!b.ax[0].cpK) {
+      if (vmax <= 8) launch_csum_v<8>(b, nchunk, nbands, deriv, mode1d, sc, s);
+      else launch_csum_lds(b, nchunk, nbands, deriv, mode1d, vmax, sc, s);
+    }
     launch_pg_c<MATERN, COS, true>(b, naxes, bpa, q, deriv, mode1d, sc, s);
   } else {
     launch_pg_c<MATERN, COS, false>(b, naxes, bpa, q, deriv, mode1d, sc, s);
@@ -695,6 +704,10 @@ hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int nax
     int T = a[k].p / 32;
     b.tiles[k] = T * (T + 1) / 2;
     if ((a[k].cls.ncls > 0) != (a[0].cls.ncls > 0) || a[k].cls.vmax > CLS_VMAX) return hipErrorInvalidValue;
+    // class tile partials on every axis or none, from GEMM epilogues (2D class path)
+    if ((a[k].cpK != nullptr) != (a[0].cpK != nullptr) ||
+        (a[k].cpK && (!a[k].cpD || a[k].cslots <= 0 || a[k].cls.ncls <= 0 || mode1d)))
+      return hipErrorInvalidValue;
   }
   b.naxes = naxes;
   b.bpa = blocks_per_axis;

@@ -155,6 +155,12 @@ class DeviceSolver:
             out.append(int(c.value))
         return out
 
+    def class_sums_in_epilogue(self):
+        """True when the G_K / G_D GEMM epilogues write the class partials (gpk_class_sum_path)."""
+        v = ctypes.c_int32()
+        check(_lib.load().gpk_class_sum_path(self._h, ctypes.byref(v)))
+        return bool(v.value)
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.load().gpk_destroy(self._h)

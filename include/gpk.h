@@ -144,6 +144,10 @@ typedef struct gpk_problem {
 /* Large 2D factors: refine only the axis-1 forward solve A = K1^{-1} U (not Bt = U K2^{-1}), as
  * the default does when beta >= 16 (advection); diagnostics (tools/c5_refine_diag.py). */
 #define GPK_FLAG_REFINE_FWD1_ONLY 2097152
+/* 2D factors with distance classes: the class sums of G_K / G_D by a class-sum launch over their
+ * rows (default: the 16x16-tile GEMMs that produce them sum each output tile per class in their
+ * epilogue, and the contraction adds those partials -- one launch fewer per step). */
+#define GPK_FLAG_NO_CLASS_BINS 4194304
 
 typedef struct gpk_handle gpk_handle;
 
@@ -210,6 +214,10 @@ int gpk_graph_mode(const gpk_handle* h, int32_t* fast, int64_t* rollbacks);
  * gpk_class_count: the classes a handle's step uses on axis 0 / 1 (0 = per-pair kernels). */
 int gpk_distance_classes(const double* x, int32_t n, int32_t* ncls, int32_t* vmax);
 int gpk_class_count(const gpk_handle* h, int32_t axis, int32_t* ncls);
+/* How a 2D class-path step sums G_K / G_D per class: *epilogue = 1 when the GEMMs that produce
+ * them write class tile partials (GPK_FLAG_NO_CLASS_BINS off, <= 16 variants per diagonal,
+ * 16x16-tile GEMM stages, unsharded), 0 when a class-sum launch reads the matrices. */
+int gpk_class_sum_path(const gpk_handle* h, int32_t* epilogue);
 
 /* Latency-tuning probes (libgpk_trace.so, `make trace`; the product library returns GPK_EINVAL):
  * per timeline slot (csrc/gpk_trace.h) the first-arrival / last-departure device clock

@@ -99,7 +99,46 @@ def test_c4_size_class_counts():
     prob, params, _, fs = problem_2d(n1=256, n2=256, Q=30, seed=0)
     s = device_solver(prob, 30, fs)
     assert s.class_counts() == [1297, 1297]
+    assert s.class_sums_in_epilogue()  # 9 variants per diagonal at most: the GEMM epilogue path
     s.close()
+
+
+# The class sums of G_K / G_D formed in the epilogues of the GEMMs that produce them (default,
+# gpk.h GPK_FLAG_NO_CLASS_BINS) against the class-sum launch: the same pairs summed in another
+# order, so the kernel-parameter gradients agree to rounding, everything else bitwise (the loss
+# and dL/dU never read the class sums).  Padded axes (72 x 40 -> 96 x 64), the D_x1 sign
+# (advection), Allen-Cahn, and C4's size (9 variants on some diagonals: the v + 8 slots).
+@pytest.mark.parametrize("eq,kind,n1,n2", [("poisson", "Matern52_Cos_1d", 72, 40),
+                                           ("advection", "Matern52_Cos_1d", 72, 40),
+                                           ("allencahn", "SE_Cos_1d", 72, 40),
+                                           ("poisson", "Matern52_Cos_1d", 256, 256)])
+def test_epilogue_class_sums_match_class_sum_launch(eq, kind, n1, n2):
+    from gpk._lib import GPK_FLAG_NO_CLASS_BINS
+    Q = 30 if n1 == 256 else 6
+    prob, params, _, fs = problem_2d(eq=eq, kind=kind, n1=n1, n2=n2, Q=Q, seed=3)
+    a = device_solver(prob, Q, fs)
+    b = device_solver(prob, Q, fs, flags=GPK_FLAG_NO_CLASS_BINS)
+    try:
+        assert a.class_sums_in_epilogue() and not b.class_sums_in_epilogue()
+        for s in (a, b):
+            s.set_params(params)
+        la, ga = a.loss_grad()
+        lb, gb = b.loss_grad()
+        assert la == lb
+        m = _u_mask(prob, params)
+        assert np.array_equal(ga[m], gb[m])
+        assert rel(ga[~m], gb[~m]) < 1e-10, rel(ga[~m], gb[~m])
+        # and after steps (the step graph's own stages): trajectories within rounding (Adam's
+        # normalised steps amplify last-bit differences of near-zero gradient components: the
+        # class-path-vs-pairs budget above)
+        ta, tb = a.step(10), b.step(10)
+        assert np.max(np.abs(ta - tb) / np.abs(tb)) < 1e-9
+        assert rel(a.get_flat(), b.get_flat()) < 1e-8
+    finally:
+        a.close()
+        b.close()
+    if n1 < 256:
+        _cmp_lossgrad(prob, params, Q, fs)  # and the oracle (the default path)
 
 
 
