@@ -396,30 +396,41 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
   if (d.vscale) alpha *= sc->v;
   if (d.vscale2) alpha2 *= sc->v;
   const double vv = d.Y ? sc->v : 0.0;
-  double red = 0.0, red2 = 0.0, cval;
+  double red = 0.0, red2 = 0.0, c;
+  const int row = i0 + (lane >> 4) + 4 * wv, col = j0 + (lane & 15);
   {
     const int q = lane * 4 + wv;
     const double s1 = (part[0][0][q] + part[0][1][q]) + (part[0][2][q] + part[0][3][q]);
-    const int row = i0 + (lane >> 4) + 4 * wv, col = j0 + (lane & 15);
-    double c = alpha * s1;
+    c = alpha * s1;
     if (DUAL && d.K2) c += alpha2 * ((part[1][0][q] + part[1][1][q]) + (part[1][2][q] + part[1][3][q]));
     c = epi_apply(d, c, ein, red, red2);
-    d.C[(size_t)row * d.ldc + col] = c;
-    epi_side(d, row, col, c, ein, vv);
-    cval = c;
   }
+  // The tile's class sums (d.cpart) and loss partials (d.red / d.red2) go through LDS: their
+  // LDS writes and ONE barrier come before this lane's global stores, because a barrier
+  // (__syncthreads: a workgroup release) waits for every earlier store of the wave to be
+  // acknowledged -- after the C store it cost a memory round trip per launch.
+  // class sums: the tile in LDS diagonal-major, element (r, c) at [r - c + 15][r], so the
+  // thread of diagonal offset dl reads its row of 16 with 16-byte loads (the 8 threads of one
+  // diagonal share it: a broadcast); positions off the diagonal's range are masked by r.  Row
+  // strides 18 doubles / 20 ints: the 16 lanes of one tile row write 16 distinct bank pairs
+  // (a 16-double stride put them on 2)
+  constexpr int BVS = 18, BWS = 20;
+  double* bv = smem + 2 * 4 * 256 + 512;              // [31][BVS] values
+  int* bvar = reinterpret_cast<int*>(bv + 31 * BVS);  // [31][BWS] variants
+  double* sred = smem + 2 * 4 * 256;                 // [2][256] loss partials
+  if (d.cpart) {  // (uniform)
+    const int r = (lane >> 4) + 4 * wv, dg = r - (lane & 15) + 15;
+    bv[dg * BVS + r] = (d.bsx && !(bxi - bxj >= 0.0)) ? -c : c;  // D_x1: s_ij G_D (JAX abs'(0) = +1)
+    bvar[dg * BWS + r] = bu >= 0 ? bu - bcb : -1;
+  }
+  if (d.red || d.red2) {  // (uniform) (past `part`, which other waves may still be reading)
+    sred[wv * 64 + lane] = red;
+    sred[256 + wv * 64 + lane] = red2;
+  }
+  if (d.cpart || d.red || d.red2) __syncthreads();  // (uniform)
+  d.C[(size_t)row * d.ldc + col] = c;
+  epi_side(d, row, col, c, ein, vv);
   if (d.cpart) {  // (uniform) the tile's sums per (signed diagonal, variant), rows in order
-    // the tile in LDS diagonal-major: element (r, c) at [r - c + 15][r], so the thread of
-    // diagonal offset dl reads its row of 16 with 16-byte loads (8 threads of one diagonal share
-    // it: a broadcast); positions off the diagonal's range are masked by r, never read as data
-    double* bv = smem + 2 * 4 * 256 + 512;                 // [31][16] values
-    int* bvar = reinterpret_cast<int*>(bv + 31 * 16);      // [31][16] variants
-    {
-      const int r = (lane >> 4) + 4 * wv, c = lane & 15, e = (r - c + 15) * 16 + r;
-      bv[e] = (d.bsx && !(bxi - bxj >= 0.0)) ? -cval : cval;  // D_x1: s_ij G_D (JAX abs'(0) = +1)
-      bvar[e] = bu >= 0 ? bu - bcb : -1;
-    }
-    __syncthreads();
     // this thread's slots: class (k, v) [and (k, v + 8)] at (sign, band group, tile row)
     const int dl = (t >> 3) - 15, v = t & 7;
     int bslot = -1, bslot2 = -1;
@@ -435,8 +446,8 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
     if (bslot >= 0) {  // (bslot2 >= 0 only if bslot is)
       typedef double d2v __attribute__((ext_vector_type(2)));
       typedef int i4v __attribute__((ext_vector_type(4)));
-      const d2v* rv = reinterpret_cast<const d2v*>(bv + (dl + 15) * 16);
-      const i4v* rw = reinterpret_cast<const i4v*>(bvar + (dl + 15) * 16);
+      const d2v* rv = reinterpret_cast<const d2v*>(bv + (dl + 15) * BVS);
+      const i4v* rw = reinterpret_cast<const i4v*>(bvar + (dl + 15) * BWS);
       double x[16];
       int w[16];
 #pragma unroll
@@ -461,24 +472,18 @@ void gemm_small_kernel(GemmBatch batch, const StepScalars* __restrict__ sc) {
       if (bslot2 >= 0) d.cpart[bslot2] = s2;
     }
   }
-  if (d.red || d.red2) {  // (uniform) the tile's partials: waves' terms in row order, then lanes
-    double* sred = smem + 2 * 4 * 256;  // (past `part`, which other waves may still be reading)
-    sred[wv * 64 + lane] = red;
-    sred[256 + wv * 64 + lane] = red2;
-    __syncthreads();
-    if (wv == 0) {
-      red = ((sred[lane] + sred[64 + lane]) + sred[128 + lane]) + sred[192 + lane];
-      red2 = ((sred[256 + lane] + sred[320 + lane]) + sred[384 + lane]) + sred[448 + lane];
-      if (d.red) {
+  if ((d.red || d.red2) && wv == 0) {  // the tile's partials: waves' terms in row order, then lanes
+    red = ((sred[lane] + sred[64 + lane]) + sred[128 + lane]) + sred[192 + lane];
+    red2 = ((sred[256 + lane] + sred[320 + lane]) + sred[384 + lane]) + sred[448 + lane];
+    if (d.red) {
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) red += __shfl_xor(red, o, 64);
-        if (lane == 0) d.red[tile] = red;
-      }
-      if (d.red2) {
+      for (int o = 32; o > 0; o >>= 1) red += __shfl_xor(red, o, 64);
+      if (lane == 0) d.red[tile] = red;
+    }
+    if (d.red2) {
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) red2 += __shfl_xor(red2, o, 64);
-        if (lane == 0) d.red2[tile] = red2;
-      }
+      for (int o = 32; o > 0; o >>= 1) red2 += __shfl_xor(red2, o, 64);
+      if (lane == 0) d.red2[tile] = red2;
     }
   }
   if (TR_FIRST) TR_HI(tslot);

@@ -47,6 +47,7 @@ for k in range(16):
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C4")
 ap.add_argument("--steps", type=int, default=5)
+ap.add_argument("--flags", type=int, default=0, help="GPK_FLAG_* bits of the handle")
 a = ap.parse_args()
 if a.config in ("C1", "C2"):  # 1D: gpk_trace.h SLOT_MCP_IN / SLOT_MCP_OUT reuse the GEMM / update slots
     for k in range(16):
@@ -61,7 +62,7 @@ if "GPK_LIB_PATH" not in os.environ:
 from gpk import _lib, problems  # noqa: E402
 
 lib = _lib.load()
-s = problems.make_solver(a.config, seed=0)
+s = problems.make_solver(a.config, seed=0, flags=a.flags)
 s.step(20)
 U64 = ctypes.c_uint64 * NS
 who = []
@@ -102,7 +103,7 @@ for _ in range(a.steps):
             acc_lo[i] += (lo[i] - t0) / 100.0 if valid_lo[i] else np.nan
             acc_hi[i] += (hi[i] - t0) / 100.0 if hi[i] > 0 else np.nan
             cnt[i] += 1
-print(f"{a.config}: one step, device timeline (us, mean of {a.steps})")
+print(f"{a.config} flags {a.flags}: one step, device timeline (us, mean of {a.steps})")
 for i in sorted(range(NS), key=lambda i: (acc_lo[i] / max(cnt[i], 1)) if cnt[i] and not np.isnan(acc_lo[i]) else 1e9):
     if cnt[i]:
         l, h = acc_lo[i] / cnt[i], acc_hi[i] / cnt[i]
