@@ -855,11 +855,12 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
     }
     __builtin_amdgcn_wave_barrier();
   };
-  // stores of every publishing tile (sc1, not waited for here)
-  auto publish_stores = [&](int kk) {
+  // stores of the publishing tiles (sc1, not waited for here): which = 0 the pivot chain's input
+  // tiles (granules, and their panel slots when they publish), 1 the other publishing tiles
+  auto publish_stores = [&](int kk, int which) {
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
-      if (!valid(s) || !chain_in(s, kk)) continue;
+      if (which != 0 || !valid(s) || !chain_in(s, kk)) continue;
       int I, J;
       multi_slot(s, R, c0, I, J);
       if (I == J) {
@@ -874,7 +875,7 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
     }
 #pragma unroll
     for (int s = 0; s < 7; ++s) {
-      if (!valid(s) || !publishes(s, kk)) continue;
+      if (!valid(s) || !publishes(s, kk) || chain_in(s, kk) != (which == 0)) continue;
       int I, J;
       multi_slot(s, R, c0, I, J);
       if (I == kk) {
@@ -888,7 +889,10 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
       }
     }
   };
-  if (!master) publish_stores(0);
+  if (!master) {
+    publish_stores(0, 0);
+    publish_stores(0, 1);
+  }
   // this workgroup's share of the other half's reset: [rs0, rs1), a chunk per sweep
   const size_t ntot = hs;
   const int gidx = (int)blockIdx.x - ((int)blockIdx.x > mpos ? 1 : 0);
@@ -1041,11 +1045,16 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
     // stores, then the rest.  (Forming V_I^T V_J as P_I^T (M_k P_J), M_k = L_k^{-T} L_k^{-1},
     // halves the V products but moved no sweep: the critical merged workgroups keep 4 products,
     // and the 5-step C2 trajectory drifted past the oracle budget -- measured, reverted.)
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
+    // pass 0: the pivot chain's input tiles (its next hop waits on them), stored at once; pass 1:
+    // the other tiles that publish panel row k + 1; pass 2: the rest.  (A loop: unrolled three
+    // times it spilled 108 B per lane.)
+#pragma unroll 1
+    for (int pass = 0; pass < 3; ++pass) {
 #pragma unroll
       for (int s = 0; s < 7; ++s) {
-        if (!valid(s) || (publishes(s, k + 1) || chain_in(s, k + 1)) != (pass == 0)) continue;
+        if (!valid(s)) continue;
+        const int ps = chain_in(s, k + 1) ? 0 : publishes(s, k + 1) ? 1 : 2;
+        if (ps != pass) continue;
         int I, J;
         multi_slot(s, R, c0, I, J);
         const double* VI = sV + (s < 4 ? (s >> 1) : (s == 4 ? 0 : 1)) * 1024;
@@ -1067,11 +1076,11 @@ __global__ __launch_bounds__(256, 2) void chain_multi_kernel(ChainBatch b) {
           acc[s] = acc[s] - prod;
         }
       }
-      if (pass == 0 && trc) TR_HI(SLOT_MC_PROD + k);
-      if (pass == 0 && k + 1 < T) publish_stores(k + 1);
-      if (pass == 0 && trc) TR_HI(SLOT_MC_PUB + k);
-      if (pass == 0 && pubk) { TR_LO(SLOT_MCP_OUT + k); TR_HI(SLOT_MCP_OUT + k); TR_WHO(SLOT_MCP_WHO_OUT + k, blockIdx.x); }
-      if (pass == 0) __builtin_amdgcn_s_setprio(0);
+      if (pass == 1 && trc) TR_HI(SLOT_MC_PROD + k);
+      if (pass < 2 && k + 1 < T) publish_stores(k + 1, pass);
+      if (pass == 1 && trc) TR_HI(SLOT_MC_PUB + k);
+      if (pass == 1 && pubk) { TR_LO(SLOT_MCP_OUT + k); TR_HI(SLOT_MCP_OUT + k); TR_WHO(SLOT_MCP_WHO_OUT + k, blockIdx.x); }
+      if (pass == 1) __builtin_amdgcn_s_setprio(0);
     }
     {  // reset chunk k of this workgroup's share of the other half
       const size_t b0 = rs0 + (size_t)k * rchunk, b1 = std::min(rs1, b0 + rchunk);
