@@ -26,32 +26,8 @@ GPK_WAIT_LIMIT_SETTER(wait_limit_assemble)  // gpk_set_wait_limit
 
 GPK_TRACE_TU(assemble)
 
-// Partial sums over components c = c0, c0 + cs, ... (cs = stride) of K and D at one pair.
-template <bool MATERN, bool COS, int DERIV>
-__device__ __forceinline__ void eval_kd_part(double diff, const double* w, const double* a,
-                                             const double* om, const double* oml, int c0, int cs,
-                                             int q, double& K, double& D) {
-  double d = fabs(diff);
-  double k = 0.0, dv = 0.0;
-  for (int c = c0; c < q; c += cs) {
-    double m0, m1, m2;
-    radial<MATERN>(d, a[c], m0, m1, m2);
-    if (COS) {
-      double S, C;
-      phase_sincos(om[c], oml[c], d, S, C);
-      double o = om[c];
-      k += w[c] * (m0 * C);
-      if (DERIV == 2) dv += w[c] * (m2 * C - 2.0 * m1 * (o * S) - m0 * (o * o * C));
-      if (DERIV == 1) dv += w[c] * (m1 * C - m0 * (o * S));
-    } else {
-      k += w[c] * m0;
-      if (DERIV == 2) dv += w[c] * m2;
-      if (DERIV == 1) dv += w[c] * m1;
-    }
-  }
-  K = k;
-  D = dv;  // unsigned: the D_x1 sign s_ij is applied by the caller
-}
+// (eval_kd_part, class_value_store: prep_dev.h, shared with the pipelined class values of the
+// parameter-gradient launch)
 
 template <bool MATERN, bool COS, int DERIV>
 __device__ __forceinline__ void eval_kd(double diff, const double* w, const double* a,
@@ -190,18 +166,8 @@ __global__ __launch_bounds__(256) void class_eval_kernel(AssembleBatch b, int q)
   __syncthreads();
   if (TR_FIRST) TR_LO(SLOT_CLASS_EVAL);
   if (TR_LAST) TR_LO(SLOT_CEVAL_START);
-  const int c = t & 31, u = blockIdx.x * 8 + (t >> 5);
-  double kv = 0.0, dv = 0.0;
-  if (u < C.ncls) eval_kd_part<MATERN, COS, DERIV>(C.dist[u], sw, sa, so, sol, c, 32, q, kv, dv);
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) {
-    kv += __shfl_xor(kv, o, 64);
-    dv += __shfl_xor(dv, o, 64);
-  }
-  if (c == 0 && u < C.ncls) {
-    C.kval[u] = kv;
-    C.dval[u] = dv;
-  }
+  const int u = blockIdx.x * 8 + (t >> 5);
+  class_value_store<MATERN, COS, DERIV>(C, u, u < C.ncls ? C.dist[u] : 0.0, sw, sa, so, sol, q);
   if (TR_FIRST) TR_HI(SLOT_CLASS_EVAL);
   if (TR_LAST) TR_HI(SLOT_CEVAL_START);
 }

@@ -193,6 +193,13 @@ struct gpk_handle {
   double* snap = nullptr;  // [3 * nparams] params, m, v at the start of a fast batch
   int* snap_count = nullptr;
   unsigned int* viol = nullptr;  // the fast graph met an open refinement gate
+  // pipelined class values (TailArgs::nce_flag): the parameter-gradient launch of step s of a
+  // captured batch evaluates step s + 1's class values after the kernel-parameter Adam.
+  // cls_next: the step being enqueued does that; cls_have: the previous enqueued step did, so
+  // this one needs no class-value launch.  Both false outside a multi-step capture.
+  unsigned int* nce_flag = nullptr;  // raised by the Adam block, reset by the next publish_prep
+  double* nce_kp = nullptr;          // [nsmall] the kernel parameters it hands over (sc1)
+  bool cls_next = false, cls_have = false;
   double* rep_host = nullptr;    // [8 + LOSS_CAP] pinned: status, viol, gates, losses (step_report)
   double* pend_losses = nullptr; // caller's buffer for the last batch's losses (finish_batch)
   int pend_n = 0;
@@ -253,7 +260,17 @@ static PrepArgs make_prep(gpk_handle* h, int apply) {
   P.dim = L.dim; P.n1 = L.n1; P.n2 = L.n2; P.p2 = L.p2;
   P.bgap = h->bgap;
   P.bgap_parts = h->bgap_parts;
+  P.nce_flag = h->nce_flag;
   return P;
+}
+
+// Pipelined class values (gpk.h GPK_FLAG_NO_CLASS_PIPE): chain-inverse handles with distance
+// classes, unsharded -- the class-value launch is then the step's only user of the kernel
+// parameters before the inverse, so it can run at the end of the previous step's parameter-
+// gradient launch, which has just updated them.
+static bool cls_pipe_ok(const gpk_handle* h) {
+  return !h->shard && h->chain && h->cls[0].ncls > 0 && h->nce_flag &&
+         !(h->prob.flags & GPK_FLAG_NO_CLASS_PIPE);
 }
 
 static void fill_spd(gpk_handle* h, SpdArgs* sa) {
@@ -321,7 +338,7 @@ static hipError_t launch_inverse(gpk_handle* h, SpdArgs* sa, double** fin, bool 
 static int split_broadcast(gpk_handle* h);  // (after ShardComm)
 
 // assemble K, D (+ step constants, + pivot block 0) and invert K: the first part of a step
-static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
+static int enqueue_assemble_inverse(gpk_handle* h, int apply, bool have_cls = false) {
   const Layout& L = h->L;
   AssembleArgs aa[2] = {};
   int deriv = (h->prob.eq == GPK_ADVECTION) ? 1 : 2;
@@ -356,8 +373,10 @@ static int enqueue_assemble_inverse(gpk_handle* h, int apply) {
     prep.viol0 = b.viol; prep.slot0 = b.loss_slot;
     h->fold_begin = nullptr;
   }
-  TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, prep_eval, h->s, eval_only),
-                   "assemble"));
+  // (have_cls: the previous step's parameter-gradient launch evaluated them, cls_pipe_ok)
+  if (!(eval_only && have_cls))
+    TRY(check_launch(launch_assemble(h->prob.kind, L.q, aa, L.naxes, prep_eval, h->s, eval_only),
+                     "assemble"));
   mark(h, 1);
   SpdArgs sa[2];
   fill_spd(h, sa);
@@ -419,6 +438,11 @@ static TailArgs make_tail(gpk_handle* h, int apply, bool refine = true) {
   T.gcount = h->tcount; T.top = h->ttop; T.gpart = h->tgpart; T.pg = h->pg;
   T.tg = h->ttg; T.ngpa = h->tngpa;
   T.gpart_lo = h->pg_dd ? h->tgpart_lo : nullptr;
+  if (h->cls_next && cls_pipe_ok(h)) {  // the next step's class values, after the Adam
+    T.nce_flag = h->nce_flag;
+    T.nce_status = h->status;
+    f.kp_wt = h->nce_kp;
+  }
   return T;
 }
 
@@ -443,9 +467,13 @@ static int launch_stage(gpk_handle* h, int k) {
 static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
   if (h->shard) return enqueue_step_shard(h, apply);
   const Layout& L = h->L;
+  // pipelined class values: this step's were evaluated by the previous step (have); this step
+  // evaluates the next one's when its caller asked for it (cls_next, make_tail)
+  const bool have = h->cls_have && cls_pipe_ok(h);
+  h->cls_have = false;
   if (h->profiling) (void)hipEventRecord(h->ev[0], h->s);
   mark(h, 0);  // "prep" is fused into the assembly launch (stage kept for the name table)
-  TRY(enqueue_assemble_inverse(h, apply));
+  TRY(enqueue_assemble_inverse(h, apply, have));
   int stage = 3;
   const char* const* names = L.dim == 2 ? kStageNames2D : kStageNames1D;
   for (int k = 0; k < 3; ++k) h->sname[k] = names[k];
@@ -483,6 +511,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
     }
     TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 0, pa, 2, h->bpa, h->sc, h->s, &tail), "pgrad"));
+    h->cls_have = tail.nce_flag != nullptr;
     stamp("pgrad_tail");
   } else {
     const int P = L.p1;
@@ -527,6 +556,7 @@ static int enqueue_step(gpk_handle* h, int apply, bool refine = true) {
     pa.part_lo = h->pg_dd ? h->pgpart_lo : nullptr;
     TailArgs tail = make_tail(h, apply, refine);
     TRY(check_launch(launch_pgrad(h->prob.kind, L.q, 1, &pa, 1, h->bpa, h->sc, h->s, &tail), "pgrad"));
+    h->cls_have = tail.nce_flag != nullptr;
     stamp("pgrad_tail");
   }
   h->nstage = stage;
@@ -1136,7 +1166,12 @@ static int capture(gpk_handle* h, int apply, bool refine = true, int reps = 1, b
   hipGraph_t g = nullptr;
   HIPCHK(hipStreamBeginCapture(h->s, hipStreamCaptureModeThreadLocal));
   int rc = GPK_OK;
-  for (int r = 0; r < reps && rc == GPK_OK; ++r) rc = enqueue_step(h, apply, refine);
+  h->cls_have = false;
+  for (int r = 0; r < reps && rc == GPK_OK; ++r) {
+    h->cls_next = r + 1 < reps;  // (cls_pipe_ok decides)
+    rc = enqueue_step(h, apply, refine);
+  }
+  h->cls_next = h->cls_have = false;
   hipError_t e = hipStreamEndCapture(h->s, &g);
   if (rc != GPK_OK) {
     if (g) (void)hipGraphDestroy(g);
@@ -1226,10 +1261,13 @@ static int capture_calln(gpk_handle* h, int reps) {
   b.loss_slot = h->loss_slot;
   const StepReport rep = make_report(h, true, reps);
   int rc = begin_batch(h, &b);
+  h->cls_have = false;
   for (int r = 0; r < reps && rc == GPK_OK; ++r) {
     if (r == reps - 1 && !h->shard) h->fold_report = &rep;
+    h->cls_next = r + 1 < reps;  // (cls_pipe_ok decides)
     rc = enqueue_step(h, 1, false);
   }
+  h->cls_next = h->cls_have = false;
   rc = end_batch(h, &rep, rc);
   hipError_t e = hipStreamEndCapture(h->s, &g);
   if (rc != GPK_OK) {
@@ -1266,6 +1304,7 @@ static int reset_handoffs(gpk_handle* h) {
     HIPCHK(hipMemsetAsync(h->cflags[a], 0, nflags * sizeof(unsigned int), h->s));
     HIPCHK(hipMemsetAsync(h->aflag[a], 0, (4 + P / 32) * sizeof(unsigned int), h->s));
   }
+  HIPCHK(hipMemsetAsync(h->nce_flag, 0, sizeof(unsigned int), h->s));
   HIPCHK(hipStreamSynchronize(h->s));
   return GPK_OK;
 }
@@ -1735,6 +1774,8 @@ static int create_impl(const gpk_problem* p, double freq_scale, int rank, int nr
   A_(h->snap, (size_t)3 * L.nparams);
   A_(h->snap_count, 1);
   A_(h->viol, 1);
+  A_(h->nce_flag, 1);
+  A_(h->nce_kp, (size_t)L.nsmall);
   if (hipHostMalloc(reinterpret_cast<void**>(&h->rep_host), (8 + LOSS_CAP) * sizeof(double),
                     hipHostMallocCoherent) != hipSuccess)
     return bail(fail(GPK_ENOMEM, "hipHostMalloc (step report)"));
@@ -2304,6 +2345,12 @@ int gpk_class_sum_path(const gpk_handle* h, int32_t* epilogue) {
   return GPK_OK;
 }
 
+int gpk_class_pipe(const gpk_handle* h, int32_t* on) {
+  if (!h || !on) return fail(GPK_EINVAL, "bad argument");
+  *on = cls_pipe_ok(h) ? 1 : 0;
+  return GPK_OK;
+}
+
 int gpk_set_spd_big_workgroups(int32_t workgroups) {
   if (workgroups < 0) return fail(GPK_EINVAL, "workgroups must be >= 0");
   spd_big_set_workgroups(workgroups);
@@ -2319,7 +2366,7 @@ int gpk_set_wait_limit(int32_t polls) {
   if (polls < 0) return fail(GPK_EINVAL, "polls must be >= 0");
   const unsigned v = polls > 0 ? (unsigned)polls : SPIN_CAP;
   if (wait_limit_spdinv(v) != hipSuccess || wait_limit_spdbig(v) != hipSuccess ||
-      wait_limit_assemble(v) != hipSuccess)
+      wait_limit_assemble(v) != hipSuccess || wait_limit_pgrad(v) != hipSuccess)
     return fail(GPK_EHIP, "set the wait limit");
   return GPK_OK;
 }

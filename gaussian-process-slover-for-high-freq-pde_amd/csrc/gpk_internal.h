@@ -151,6 +151,9 @@ struct PrepArgs {
   // rollback snapshot of (params, m, v) copied by the publishing launch's spare workgroups
   int* snap_count; unsigned int* viol0; int* slot0;
   double* snap; const double* snap_m; const double* snap_v; size_t snap_np;
+  // pipelined class values (TailArgs::nce_flag): reset to 0 by thread 0 of publish_prep, i.e.
+  // between the previous step's parameter-gradient launch (its waiters are done) and this one's
+  unsigned int* nce_flag;
 };
 
 // Distance classes.  Every field of a stationary kernel depends on the pair (i, j) only
@@ -332,6 +335,7 @@ constexpr unsigned SPIN_CAP = 1u << 22;
 hipError_t wait_limit_spdinv(unsigned polls);
 hipError_t wait_limit_spdbig(unsigned polls);
 hipError_t wait_limit_assemble(unsigned polls);
+hipError_t wait_limit_pgrad(unsigned polls);
 hipError_t launch_spd_inverse_big(SpdArgs* args, int nmat, double** final_out, hipStream_t s);
 // stage -1: pivot 0; 2k: panel of sweep k; 2k+1: update of sweep k
 // (mirror = false: the last update launch leaves the upper triangle unmirrored -- bench timing)

@@ -20,9 +20,12 @@
 #include "gpk_internal.h"
 #include "gpk_trace.h"
 #include "fields_dd.h"
+#include "spd_pivot.h"
+#include "prep_dev.h"
 
 namespace gpk {
 GPK_TRACE_TU(pgrad)
+GPK_WAIT_LIMIT_SETTER(wait_limit_pgrad)  // gpk_set_wait_limit
 }  // namespace gpk
 #define FIN_PROBE(slot) TR_HI(slot)  // finalize_body phases (gpk_trace.h)
 #include "stepk_dev.h"
@@ -174,6 +177,38 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
   if (t == 0) TR_HI(SLOT_PG_TOP);
   finalize_body(T.fin, 2);  // (the loss part ran at the start of the launch)
   if (t == 0) TR_HI(SLOT_PG_FINAL);
+  if (T.nce_flag) {  // the updated kernel parameters (fin.kp_wt, sc1) -> the next step's class values
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave drains its sc1 stores
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(T.nce_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Pipelined class values (TailArgs::nce_flag; gpk_api.cpp cls_pipe_ok): plane naxes + 2 + ax of
+// the launch evaluates the NEXT step's class values of axis ax -- the same 8 classes per
+// workgroup and the same code as class_eval_kernel (class_value_store), from the parameters the
+// kernel-parameter Adam of this launch has just written: bitwise the values the next step's
+// class-value launch would produce, which that step then skips.  These workgroups are the last
+// of the grid: the block they wait for (the last contraction block to arrive) was dispatched
+// before them and waits for none of them, so the wait cannot deadlock at any grid size.
+template <bool MATERN, bool COS, int DERIV>
+__device__ void next_class_values(const PGradBatch& b, int ax, int blk, int q) {
+  const ClassArgs& C = b.ax[ax].cls;
+  if (blk * 8 >= C.ncls) return;
+  __shared__ double sw[QMAX], sa[QMAX], so[QMAX], sol[QMAX];
+  const int t = threadIdx.x, u = blk * 8 + (t >> 5);
+  const double d = u < C.ncls ? C.dist[u] : 0.0;  // (issued before the wait)
+  // the guide's sc1 hand-off (no fences): thread 0 polls the flag with sc1 loads, the barrier,
+  // then sc1 loads of the parameters the Adam block stored write-through
+  if (t == 0) (void)spin_until_ge<1>(b.tail.nce_flag, 1u, b.tail.nce_status);  // bounded: status bit 2
+  __syncthreads();
+  if (t < q) {
+    const Layout& L = b.tail.fin.L;
+    const double* kp = b.tail.fin.kp_wt + ((ax == 0 ? L.off_kp[0] : L.off_kp[1]) - L.off_small);
+    axis_component_v(ld_wt(kp + t), ld_wt(kp + q + t), ld_wt(kp + 2 * q + t), sw[t], sa[t], so[t], sol[t]);
+  }
+  __syncthreads();
+  class_value_store<MATERN, COS, DERIV>(C, u, d, sw, sa, so, sol, q);
 }
 
 // ---- class path (gpk_internal.h ClassArgs) -------------------------------------------------
@@ -415,6 +450,10 @@ __global__ __launch_bounds__(256) void pgrad_kernel(PGradBatch b, int q,
     if (blk == 0) finalize_body(b.tail.fin, 1);
     return;
   }
+  if (axis >= b.naxes + 2) {  // the next step's class values (pipelined)
+    if (CLS && b.tail.nce_flag) next_class_values<MATERN, COS, DERIV>(b, axis - (b.naxes + 2), blk, q);
+    return;
+  }
   if (axis == b.naxes) {
     if (threadIdx.x == 0 && blk == 0) TR_LO(SLOT_PG_UPLANE);  // fused tail: dL/dU + Adam on U (grid-stride over the solution grid)
     const int nu = tail_nu(b.tail.adam.L);
@@ -651,6 +690,10 @@ static void launch_pg_c(const PGradBatch& b, int naxes, int bpa, int q, int deri
   // the U plane (dL/dU + Adam) gets one element per thread when it is wider than bpa blocks
   const int ublocks = b.tail.fused ? (tail_nu(b.tail.adam.L) + 255) / 256 : 0;
   dim3 grid(std::max(bpa, std::min(ublocks, 4096)), naxes + (b.tail.fused ? 2 : 0));
+  if (b.tail.fused && b.tail.nce_flag) {  // + one plane per axis: the next step's class values
+    for (int k = 0; k < naxes; ++k) grid.x = std::max<unsigned>(grid.x, (b.ax[k].cls.ncls + 7) / 8);
+    grid.y += naxes;
+  }
   // double-double contraction: class path, 2D, with the fused tail carrying the low parts
   const bool ddc = CLS && b.tail.fused && b.tail.gpart_lo && b.ax[0].part_lo && (naxes < 2 || b.ax[1].part_lo);
   if (ddc) {
@@ -716,6 +759,10 @@ hipError_t launch_pgrad(int kind, int q, int mode1d, const PGradArgs* a, int nax
     // every block of the gradient planes must exist: group sizes are sized on bpa
     if (b.tail.tg <= 0 || b.tail.ngpa * b.tail.tg < blocks_per_axis) return hipErrorInvalidValue;
   }
+  // pipelined class values: the class path with the fused tail only (its Adam block raises the flag)
+  if (b.tail.nce_flag && (!b.tail.fused || !b.tail.nce_status || !b.tail.fin.kp_wt || a[0].cls.ncls <= 0 ||
+                          shard_n > 1))
+    return hipErrorInvalidValue;
   int deriv = a[0].deriv;
   switch (kind) {
     case SE_COS: launch_pg_t<false, true>(b, naxes, blocks_per_axis, q, deriv, mode1d, sc, s); break;

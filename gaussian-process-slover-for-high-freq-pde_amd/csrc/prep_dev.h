@@ -8,14 +8,67 @@
 namespace gpk {
 
 // exp of the params -> axis constants of component c (prep2 semantics, bitwise)
+// (from the values: freq f, log-ls ll, log-w lw)
+__device__ __forceinline__ void axis_component_v(double f, double ll, double lw, double& w, double& a,
+                                                 double& om, double& oml) {
+  om = TWO_PI * f;
+  oml = om_low(f, om);
+  a = exp(ll);
+  w = exp(lw);
+}
+
 __device__ __forceinline__ void axis_component(const PrepArgs& P, int axis, int q, int c, double& w,
                                                double& a, double& om, double& oml) {
   const int off = P.off_kp[axis];
-  const double f = P.params[off + c];       // freq
-  om = TWO_PI * f;
-  oml = om_low(f, om);
-  a = exp(P.params[off + q + c]);           // log-ls
-  w = exp(P.params[off + 2 * q + c]);       // log-w
+  axis_component_v(P.params[off + c], P.params[off + q + c], P.params[off + 2 * q + c], w, a, om, oml);
+}
+
+// Partial sums over components c = c0, c0 + cs, ... (cs = stride) of K and D at one pair.
+template <bool MATERN, bool COS, int DERIV>
+__device__ __forceinline__ void eval_kd_part(double diff, const double* w, const double* a,
+                                             const double* om, const double* oml, int c0, int cs,
+                                             int q, double& K, double& D) {
+  double d = fabs(diff);
+  double k = 0.0, dv = 0.0;
+  for (int c = c0; c < q; c += cs) {
+    double m0, m1, m2;
+    radial<MATERN>(d, a[c], m0, m1, m2);
+    if (COS) {
+      double S, C;
+      phase_sincos(om[c], oml[c], d, S, C);
+      double o = om[c];
+      k += w[c] * (m0 * C);
+      if (DERIV == 2) dv += w[c] * (m2 * C - 2.0 * m1 * (o * S) - m0 * (o * o * C));
+      if (DERIV == 1) dv += w[c] * (m1 * C - m0 * (o * S));
+    } else {
+      k += w[c] * m0;
+      if (DERIV == 2) dv += w[c] * m2;
+      if (DERIV == 1) dv += w[c] * m1;
+    }
+  }
+  K = k;
+  D = dv;  // unsigned: the D_x1 sign s_ij is applied by the caller
+}
+
+// Class u's values (class_eval_kernel; pgrad.hip next_class_values): K and the derivative field
+// at the class distance d, one mixture component per lane of a 32-lane half-wave (component c
+// and c + 32, ...), the terms added by a fixed xor butterfly (deterministic); lane 0 stores.
+template <bool MATERN, bool COS, int DERIV>
+__device__ __forceinline__ void class_value_store(const ClassArgs& C, int u, double d, const double* sw,
+                                                  const double* sa, const double* so,
+                                                  const double* sol, int q) {
+  const int c = threadIdx.x & 31;
+  double kv = 0.0, dv = 0.0;
+  if (u < C.ncls) eval_kd_part<MATERN, COS, DERIV>(d, sw, sa, so, sol, c, 32, q, kv, dv);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    kv += __shfl_xor(kv, o, 64);
+    dv += __shfl_xor(dv, o, 64);
+  }
+  if (c == 0 && u < C.ncls) {
+    C.kval[u] = kv;
+    C.dval[u] = dv;
+  }
 }
 
 // the rollback snapshot of a folded batch begin (PrepArgs.snap), spread over nwg workgroups
@@ -97,6 +150,7 @@ __device__ inline void publish_prep(const PrepArgs& P, int q, bool bgap_all = tr
     if (P.snap_count) *P.snap_count = c0;
     if (P.viol0) *P.viol0 = 0u;
     if (P.slot0) *P.slot0 = 0;
+    if (P.nce_flag) *P.nce_flag = 0u;
     if (P.apply) *P.count = n;
     P.sc->bc1 = 1.0 - pow(P.b1, (double)n);
     P.sc->bc2 = 1.0 - pow(P.b2, (double)n);

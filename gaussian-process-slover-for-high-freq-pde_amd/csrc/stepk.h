@@ -61,6 +61,10 @@ struct FinalizeArgs {
   // last step of a batch in a captured call: the loss workgroup writes the batch report itself
   // (after this step's loss), in place of a separate step_report launch
   int report; StepReport rep;
+  // nullable [nsmall]: the kernel parameters after this step's Adam (index idx - L.off_small),
+  // stored write-through (sc1) by the Adam block for the next step's class values (the guide's
+  // sc1 hand-off: pgrad.hip pgrad_tail raises TailArgs::nce_flag after them)
+  double* kp_wt;
 };
 
 struct AdamUArgs {
@@ -93,6 +97,12 @@ struct TailArgs {
   double* pg;                // [naxes][3*QMAX] reduced parameter gradients (-> fin.pg)
   int tg, ngpa;              // blocks per group, groups per axis
   double* gpart_lo;          // DD contraction: the group partials' low parts (null: fp64)
+  // pipelined class values (null: off): the launch carries naxes more planes that evaluate the
+  // NEXT step's class values (pgrad.hip next_class_values); the block that runs the kernel-
+  // parameter Adam raises *nce_flag after it (agent release), the planes wait for it (bounded,
+  // status bit 2 on a lost hand-off) and read the updated parameters
+  unsigned int* nce_flag;
+  int* nce_status;
 };
 
 hipError_t launch_step_begin(const StepBegin& b, hipStream_t s);

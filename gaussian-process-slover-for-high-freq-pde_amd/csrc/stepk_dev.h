@@ -180,6 +180,8 @@ __device__ inline void finalize_body(const FinalizeArgs& f, int part = 0) {
       adam1(g, pp[r], pm[r], pv2[r], f.hyper, bc1, bc2);
       f.params[idx] = pp[r]; f.m[idx] = pm[r]; f.v[idx] = pv2[r];
     }
+    if (f.kp_wt && pkind[r] == 0)  // global_store sc1 (write-through hand-off)
+      __hip_atomic_store(f.kp_wt + (idx - L.off_small), pp[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

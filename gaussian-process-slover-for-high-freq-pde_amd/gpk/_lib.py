@@ -35,6 +35,7 @@ GPK_FLAG_ONE_SWEEP_UPDATE = 524288
 GPK_FLAG_NO_QUARTER_FIRST = 1048576
 GPK_FLAG_REFINE_FWD1_ONLY = 2097152
 GPK_FLAG_NO_CLASS_BINS = 4194304
+GPK_FLAG_NO_CLASS_PIPE = 8388608
 GPK_INV_SWEEP, GPK_INV_CHAIN, GPK_INV_CHAIN_AUG, GPK_INV_BIG, GPK_INV_BIG_WIDE, GPK_INV_CHAIN_MULTI = range(6)
 INV_PATH_NAMES = {0: "sweep", 1: "chain", 2: "chain_aug", 3: "big", 4: "big_wide", 5: "chain_multi"}
 KIND_IDS = {"SE_Cos_1d": 0, "Matern52_Cos_1d": 1, "SE_1d": 2, "Matern52_1d": 3}
@@ -128,6 +129,7 @@ EXPORTS = {
     "gpk_distance_classes": ([_dp, ctypes.c_int32, _ip, _ip], ctypes.c_int),
     "gpk_class_count": ([ctypes.c_void_p, ctypes.c_int32, _ip], ctypes.c_int),
     "gpk_class_sum_path": ([ctypes.c_void_p, _ip], ctypes.c_int),
+    "gpk_class_pipe": ([ctypes.c_void_p, _ip], ctypes.c_int),
     "gpk_create3": ([ctypes.POINTER(gpk_problem3), ctypes.c_double,
                      ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     "gpk_destroy3": ([ctypes.c_void_p], ctypes.c_int),

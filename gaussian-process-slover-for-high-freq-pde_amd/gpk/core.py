@@ -161,6 +161,13 @@ class DeviceSolver:
         check(_lib.load().gpk_class_sum_path(self._h, ctypes.byref(v)))
         return bool(v.value)
 
+    def class_pipe(self):
+        """True when multi-step batches evaluate the next step's class values inside the
+        parameter-gradient launch (gpk_class_pipe)."""
+        v = ctypes.c_int32()
+        check(_lib.load().gpk_class_pipe(self._h, ctypes.byref(v)))
+        return bool(v.value)
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.load().gpk_destroy(self._h)

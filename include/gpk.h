@@ -148,6 +148,11 @@ typedef struct gpk_problem {
  * rows (default: the 16x16-tile GEMMs that produce them sum each output tile per class in their
  * epilogue, and the contraction adds those partials -- one launch fewer per step). */
 #define GPK_FLAG_NO_CLASS_BINS 4194304
+/* Chain-inverse handles with distance classes: every step of a multi-step batch evaluates its
+ * class values in a launch of its own (default: step s + 1's class values are evaluated at the
+ * end of step s's parameter-gradient launch, right after the kernel-parameter Adam, so steps
+ * 2.. of a batch start with the inverse launch).  Bitwise the same results; A/B only. */
+#define GPK_FLAG_NO_CLASS_PIPE 8388608
 
 typedef struct gpk_handle gpk_handle;
 
@@ -218,6 +223,10 @@ int gpk_class_count(const gpk_handle* h, int32_t axis, int32_t* ncls);
  * them write class tile partials (GPK_FLAG_NO_CLASS_BINS off, <= 16 variants per diagonal,
  * 16x16-tile GEMM stages, unsharded), 0 when a class-sum launch reads the matrices. */
 int gpk_class_sum_path(const gpk_handle* h, int32_t* epilogue);
+/* *on = 1 when a multi-step batch evaluates step s + 1's class values at the end of step s's
+ * parameter-gradient launch (chain-inverse handles with distance classes, unsharded,
+ * GPK_FLAG_NO_CLASS_PIPE off), 0 when every step launches its own class-value evaluation. */
+int gpk_class_pipe(const gpk_handle* h, int32_t* on);
 
 /* Latency-tuning probes (libgpk_trace.so, `make trace`; the product library returns GPK_EINVAL):
  * per timeline slot (csrc/gpk_trace.h) the first-arrival / last-departure device clock
