@@ -438,6 +438,9 @@ static TailArgs make_tail(gpk_handle* h, int apply, bool refine = true) {
   T.gcount = h->tcount; T.top = h->ttop; T.gpart = h->tgpart; T.pg = h->pg;
   T.tg = h->ttg; T.ngpa = h->tngpa;
   T.gpart_lo = h->pg_dd ? h->tgpart_lo : nullptr;
+  // the fused tail's Adam block forms pg from the group partials itself (the sharded path's
+  // standalone finalize reads pg: enqueue_step_shard clears these)
+  f.gpart = T.gpart; f.gpart_lo = T.gpart_lo; f.ngpa = T.ngpa; f.pg_out = h->pg;
   if (h->cls_next && cls_pipe_ok(h)) {  // the next step's class values, after the Adam
     T.nce_flag = h->nce_flag;
     T.nce_status = h->status;
@@ -1141,6 +1144,8 @@ static int enqueue_step_shard(gpk_handle* h, int apply) {
   TRY(h->comm->allreduce(h, h->sred, (size_t)(h->red_quad + h->nquad - h->sred)));
   TRY(check_launch(launch_status_f64(h->status, h->stat_x, 1, h->s), "status_unpack"));
   TailArgs T = make_tail(h, apply);
+  T.fin.gpart = T.fin.gpart_lo = nullptr;  // (pg all-reduced above)
+  T.fin.pg_out = nullptr;
   TRY(check_launch(launch_finalize(T.fin, h->s), "finalize"));
   // this rank's tile slots are rewritten next step; the summed copies must not leak into it
   HIPCHK(hipMemsetAsync(h->red_egap, 0, (size_t)h->negap * sizeof(double), h->s));

@@ -71,58 +71,7 @@ __device__ __forceinline__ bool arrive_last(unsigned int* counter, unsigned int 
   return *s_flag != 0;
 }
 
-__device__ __forceinline__ double ld_wt(const double* p) {  // global_load sc1 (L2-served)
-  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// sum_{k<n} p[k*stride] in index order (sc1 loads), 16 in flight per batch (latency-bound chain)
-__device__ __forceinline__ double strided_sum(const double* p, int stride, int n) {
-  double acc = 0.0;
-  if (n > 16 && n <= 32) {  // (C2's levels: 25-26 partials) every load in flight at once, same order
-    double v[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] = ld_wt(p + (size_t)(j < n ? j : 0) * stride);
-#pragma unroll
-    for (int j = 0; j < 32; ++j)
-      if (j < n) acc += v[j];
-    return acc;
-  }
-  int k = 0;
-  for (; k + 16 <= n; k += 16) {
-    double v[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = ld_wt(p + (size_t)(k + j) * stride);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc += v[j];
-  }
-  if (k < n) {  // remainder: one masked batch (a scalar loop here ran one round trip per load)
-    double v[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = ld_wt(p + (size_t)(k + j < n ? k + j : k) * stride);
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (k + j < n) acc += v[j];
-  }
-  return acc;
-}
-
-// the same sum of double-double values (high parts at ph, low parts at pl), in index order
-__device__ __forceinline__ dd::D strided_sum_dd(const double* ph, const double* pl, int stride, int n) {
-  dd::D acc = {0.0, 0.0};
-  for (int k = 0; k < n; k += 16) {
-    double vh[16], vl[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const size_t o = (size_t)(k + j < n ? k + j : k) * stride;
-      vh[j] = ld_wt(ph + o);
-      vl[j] = ld_wt(pl + o);
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (k + j < n) acc = dd::add(acc, dd::D{vh[j], vl[j]});
-  }
-  return acc;
-}
+// (ld_wt, strided_sum, strided_sum_dd: stepk_dev.h, shared with finalize_body)
 
 __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
   const TailArgs& T = b.tail;
@@ -159,22 +108,12 @@ __device__ void pgrad_tail(const PGradBatch& b, int axis, int blk, int q) {
   if (t == 0) TR_HI(SLOT_PG_GROUP);
   if (!arrive_last(T.top, (unsigned)(b.naxes * T.ngpa), &s_last)) return;
   if (t == 0) TR_LO(SLOT_PG_TOP);
-  // only the naxes * 3q live entries (<= 256 at Q <= 42: one batch of loads per thread; a loop
-  // over all 3 QMAX slots per axis ran two dependent batches in half the threads)
-  for (int e = t; e < b.naxes * 3 * q; e += 256) {
-    const int ax = e / (3 * q), rem = e % (3 * q);
-    const int x = (rem / q) * QMAX + rem % q;
-    if (T.gpart_lo) {
-      const dd::D acc = strided_sum_dd(T.gpart + (size_t)ax * T.ngpa * (3 * QMAX) + x,
-                                       T.gpart_lo + (size_t)ax * T.ngpa * (3 * QMAX) + x, 3 * QMAX, T.ngpa);
-      T.pg[ax * 3 * QMAX + x] = acc.h + acc.l;
-    } else {
-      T.pg[ax * 3 * QMAX + x] = strided_sum(T.gpart + (size_t)ax * T.ngpa * (3 * QMAX) + x, 3 * QMAX, T.ngpa);
-    }
-  }
-  __syncthreads();  // pg (global) written by this block is visible to it after the barrier
   if (t == 0) *T.top = 0u;
   if (t == 0) TR_HI(SLOT_PG_TOP);
+  // the kernel-parameter gradients and Adam: each thread sums its own parameters' pg entries
+  // from the group partials (FinalizeArgs::gpart, set by make_tail) together with its other
+  // loads -- one round trip (the pg of every live entry used to be summed into global pg first,
+  // then re-loaded)
   finalize_body(T.fin, 2);  // (the loss part ran at the start of the launch)
   if (t == 0) TR_HI(SLOT_PG_FINAL);
   if (T.nce_flag) {  // the updated kernel parameters (fin.kp_wt, sc1) -> the next step's class values

@@ -61,6 +61,10 @@ struct FinalizeArgs {
   // last step of a batch in a captured call: the loss workgroup writes the batch report itself
   // (after this step's loss), in place of a separate step_report launch
   int report; StepReport rep;
+  // fused tail (part 2): each thread forms its kernel parameters' pg entries itself from the
+  // group partials (gpart [naxes * ngpa][3 QMAX], + gpart_lo: double-double) in group order,
+  // with its other loads in the same round trip, and stores them to pg_out; null: read pg
+  const double* gpart; const double* gpart_lo; int ngpa; double* pg_out;
   // nullable [nsmall]: the kernel parameters after this step's Adam (index idx - L.off_small),
   // stored write-through (sc1) by the Adam block for the next step's class values (the guide's
   // sc1 hand-off: pgrad.hip pgrad_tail raises TailArgs::nce_flag after them)

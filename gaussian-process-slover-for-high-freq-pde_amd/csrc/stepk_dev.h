@@ -4,6 +4,7 @@
 #pragma once
 #include "gpk_internal.h"
 #include "stepk.h"
+#include "dd_dev.h"
 
 #ifndef FIN_PROBE
 #define FIN_PROBE(slot) ((void)0)
@@ -30,6 +31,59 @@ __device__ inline double block_sum(double v, double* sh) {
   double s = 0.0;
   for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += sh[w];
   return s;  // valid in every thread
+}
+
+__device__ __forceinline__ double ld_wt(const double* p) {  // global_load sc1 (L2-served)
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum_{k<n} p[k*stride] in index order (sc1 loads), 16 in flight per batch (latency-bound chain)
+__device__ __forceinline__ double strided_sum(const double* p, int stride, int n) {
+  double acc = 0.0;
+  if (n > 16 && n <= 32) {  // (C2's levels: 25-26 partials) every load in flight at once, same order
+    double v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = ld_wt(p + (size_t)(j < n ? j : 0) * stride);
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if (j < n) acc += v[j];
+    return acc;
+  }
+  int k = 0;
+  for (; k + 16 <= n; k += 16) {
+    double v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = ld_wt(p + (size_t)(k + j) * stride);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc += v[j];
+  }
+  if (k < n) {  // remainder: one masked batch (a scalar loop here ran one round trip per load)
+    double v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = ld_wt(p + (size_t)(k + j < n ? k + j : k) * stride);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (k + j < n) acc += v[j];
+  }
+  return acc;
+}
+
+// the same sum of double-double values (high parts at ph, low parts at pl), in index order
+__device__ __forceinline__ dd::D strided_sum_dd(const double* ph, const double* pl, int stride, int n) {
+  dd::D acc = {0.0, 0.0};
+  for (int k = 0; k < n; k += 16) {
+    double vh[16], vl[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const size_t o = (size_t)(k + j < n ? k + j : k) * stride;
+      vh[j] = ld_wt(ph + o);
+      vl[j] = ld_wt(pl + o);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (k + j < n) acc = dd::add(acc, dd::D{vh[j], vl[j]});
+  }
+  return acc;
 }
 
 // Single-workgroup tail of the step: scalars, loss, small-parameter gradients + Adam.
@@ -115,7 +169,19 @@ __device__ inline void finalize_body(const FinalizeArgs& f, int part = 0) {
     const int rr = idx - L.off_kp[a], ty = rr / L.q, c = rr % L.q;  // ty: freq, log-ls, log-w
     pkind[r] = 0;
     pw[r] = f.kc[a].w[c];
-    pgx[r] = (ty == 0 && !f.has_cos) ? 0.0 : f.pg[a * 3 * QMAX + ty * QMAX + c];
+    const int x = ty * QMAX + c;
+    double pgv;
+    if (f.gpart && f.gpart_lo) {  // (pgrad.hip pg_reduced's sums, in this thread)
+      const dd::D acc = strided_sum_dd(f.gpart + (size_t)a * f.ngpa * (3 * QMAX) + x,
+                                       f.gpart_lo + (size_t)a * f.ngpa * (3 * QMAX) + x, 3 * QMAX, f.ngpa);
+      pgv = acc.h + acc.l;
+    } else if (f.gpart) {
+      pgv = strided_sum(f.gpart + (size_t)a * f.ngpa * (3 * QMAX) + x, 3 * QMAX, f.ngpa);
+    } else {
+      pgv = f.pg[a * 3 * QMAX + x];
+    }
+    if (f.pg_out) f.pg_out[a * 3 * QMAX + x] = pgv;
+    pgx[r] = (ty == 0 && !f.has_cos) ? 0.0 : pgv;
   }
   // ---- phase 1: reductions, loss (thread 0)
   if (t == 0) FIN_PROBE(55);
